@@ -1,0 +1,235 @@
+"""Benchmark: rows/s projected (KDD2012 54,686,452 -> 4096, R from SparseRandomProjection(random_state=123)).
+
+One step = one pass of the hot path (C = A @ R, librp's single-launch HIP SpGEMM) over the whole
+workload, inputs resident in HBM when timing starts (boundary 1 of SURVEY.md §8(d)):
+  N=1: BASELINE.json configs[1] — the full KDD2012 train shape, 119,705,032 synthetic rows
+       (per-row nnz 1 + Poisson(10), distinct uniform columns, values 1.0) on one MI355X.
+  N>1: weak scaling — every rank projects its own 119,705,032-row shard (configs[2]'s
+       row-sharding), R packed once on rank 0 and broadcast over RCCL; no collective in the loop.
+Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--dist uniform|powerlaw]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes_per_row(a, rbar, c):
+    """Gustavson no-reuse model on the reference's formats (f32 values, int32
+    indices, int32 row pointers): A ptr + idx/val, R ptr pair + gathered entries, C ptr + idx/val."""
+    return (4 + 8 * a) + a * (8 + 8 * rbar) + (4 + 8 * c)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=119_705_032)
+    ap.add_argument("--m", type=int, default=54_686_452)
+    ap.add_argument("--p", type=int, default=4096)
+    ap.add_argument("--dist", choices=["uniform", "powerlaw"], default="uniform")
+    ap.add_argument("--order", choices=["scipy", "sorted"], default="scipy")
+    ap.add_argument("--cpu-sample-rows", type=int, default=8_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from randomprojection_amd import Projector, srp_matrix as sm, synth
+    from randomprojection_amd import _native as nat
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # ---- R: generated once on rank 0 (sklearn-identical), packed and uploaded, broadcast over RCCL
+    t0 = time.perf_counter()
+    R_host = None
+    if rank == 0:
+        comp = sm.sparse_random_matrix(args.p, args.m, random_state=123)
+        R_host = sm.projection_operand(comp)
+        del comp
+        P = Projector(R_host, device=local)
+        meta = {f: getattr(P.info, f) for f in ("m", "p", "nnz", "layout", "value_type", "magnitude",
+                                                "block_shift", "n_buffers")}
+        meta["buffer_bytes"] = list(P.info.buffer_bytes)
+    else:
+        meta = None
+    t_r = time.perf_counter() - t0
+    t_bcast = 0.0
+    if world > 1:
+        box = [meta]
+        dist.broadcast_object_list(box, src=0)
+        meta = box[0]
+        bufs = [torch.empty(max(int(b), 1), dtype=torch.uint8, device=dev) for b in meta["buffer_bytes"][:meta["n_buffers"]]]
+        if rank == 0:
+            P.export_image([b.data_ptr() for b in bufs])
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        for b in bufs:
+            dist.broadcast(b, src=0)          # the recipe's sc.broadcast(R), once, over xGMI
+        torch.cuda.synchronize()
+        t_bcast = time.perf_counter() - tb
+        if rank != 0:
+            info = nat.ProjectorInfo()
+            for f in ("m", "p", "nnz", "layout", "value_type", "magnitude", "block_shift", "n_buffers"):
+                setattr(info, f, meta[f])
+            for i, b in enumerate(meta["buffer_bytes"]):
+                info.buffer_bytes[i] = int(b)
+            P = Projector.from_image(info, [b.data_ptr() for b in bufs], device=local)
+        del bufs
+    log(f"[rank {rank}] R ready: layout={P.layout} nnz={P.nnz} ({t_r:.1f}s build, {t_bcast*1e3:.1f} ms bcast)")
+
+    # ---- A: this rank's synthetic shard, generated in HBM
+    t0 = time.perf_counter()
+    Ap, Aj, Ax = synth.kdd_rows_device(args.rows, args.m, seed=2012 + rank, dist=args.dist, device=local)
+    torch.cuda.synchronize()
+    nnz_a = int(Aj.numel())
+    log(f"[rank {rank}] A: {args.rows} rows, nnz={nnz_a} ({time.perf_counter() - t0:.1f}s)")
+
+    # ---- output buffers sized by an exact first run
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    ws = torch.empty(int(nat.load().rp_project_workspace_bytes(P._h, args.rows)), dtype=torch.uint8, device=dev)
+    cap = int(1.3 * nnz_a * P.nnz / P.m) + 1024
+    Cj = torch.empty(cap, dtype=torch.int32, device=dev)
+    Cx = torch.empty(cap, dtype=torch.float32, device=dev)
+    ip_dtype = torch.int32 if cap < 2**31 else torch.int64
+    Cp = torch.empty(args.rows + 1, dtype=ip_dtype, device=dev)
+    try:
+        nnz_c = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=args.order, stream=stream, workspace=ws, nnz_a=nnz_a)
+    except nat.RPError as e:
+        if e.code != nat.RP_ERR_CAPACITY:
+            raise
+        nnz_c = e.nnz
+        Cj = torch.empty(nnz_c, dtype=torch.int32, device=dev)
+        Cx = torch.empty(nnz_c, dtype=torch.float32, device=dev)
+        if nnz_c >= 2**31:
+            Cp = torch.empty(args.rows + 1, dtype=torch.int64, device=dev)
+        nnz_c = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=args.order, stream=stream, workspace=ws, nnz_a=nnz_a)
+
+    def step():
+        P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=args.order, stream=stream, workspace=ws, nnz_a=nnz_a, sync=False)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(torch.cuda.current_stream(dev))
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    e1.record(torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    t_wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    kernel_ms = e0.elapsed_time(e1) / args.steps
+    t_max = t_wall
+    if world > 1:
+        tt = torch.tensor([t_wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+
+    a = nnz_a / args.rows
+    c = nnz_c / args.rows
+    rbar = P.nnz / P.m
+    b_row = algorithmic_bytes_per_row(a, rbar, c)
+    achieved = args.rows * b_row / (kernel_ms * 1e-3) / 1e9
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, Ap, Aj, Ax, R_host)
+
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("rows") == args.rows and tj.get("dist") == args.dist:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+
+    if rank == 0:
+        total_rows = args.rows * world
+        out = {
+            "metric": "rows/sec projected (whole node), KDD2012 54.7M->4096 dims; achieved HBM GB/s",
+            "value": total_rows / (t_max / args.steps),
+            "unit": "rows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic KDD2012-shaped rows ({args.dist} columns, 1+Poisson(10) nnz/row, values 1.0), "
+                    "R = SparseRandomProjection(4096, random_state=123) regenerated bit-identically",
+            "config": {"workload": f"configs[1]: KDD2012 train {args.rows} rows x {args.m} -> {args.p} "
+                                   f"per GPU, device-resident CSR in/out",
+                       "rows_per_gpu": args.rows, "m": args.m, "p": args.p, "nnz_in": nnz_a, "nnz_out": nnz_c,
+                       "order": args.order, "r_layout": P.layout, "parallelism": f"row-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel_ms": kernel_ms, "bytes_per_row": b_row,
+                         "model": "B_row=(4+8a)+a(8+8r)+(4+8c)", "a": a, "r": rbar, "c": c},
+            "cpu_baseline": cpu,
+            "r_setup_s": t_r,
+            "r_broadcast_ms": t_bcast * 1e3,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, Ap, Aj, Ax, R_host):
+    """The oracle's C restatement of scipy csr_matmat (maxnnz + matmat, unfused) on host threads over
+    the first rows of the same workload: SURVEY.md §8(d)(ii), kind "port"."""
+    from oracle import smmp
+
+    n = min(args.cpu_sample_rows, args.rows)
+    ap = Ap[: n + 1].cpu().numpy().astype(np.int64)
+    e = int(ap[-1])
+    aj = Aj[:e].cpu().numpy()
+    ax = Ax[:e].cpu().numpy()
+    ap32 = (ap - ap[0]).astype(np.int32)
+    Bp = R_host.indptr.astype(np.int32)
+    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    smmp.project_mt(ap32[:1001], aj, ax, Bp, R_host.indices, R_host.data, R_host.shape[1], 1)  # warm
+    t0 = time.perf_counter()
+    smmp.project_mt(ap32, aj, ax, Bp, R_host.indices, R_host.data, R_host.shape[1], threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} rows of the same synthetic workload; oracle/smmp.c (scipy csr_matmat_maxnnz + "
+                      f"csr_matmat restated) on {threads} threads, {dt:.2f}s wall"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+/*
+ * rp.h — C-ABI of librp.so, the MI355X-native projection step `X_partition @ R` of
+ * afcarl/RandomProjection. Plain pointers and sizes only; no exceptions cross the ABI; every
+ * entry point returns an rp_status (0 = RP_OK) and rp_last_error() describes the last failure on
+ * the calling thread.
+ *
+ * What each entry point replaces in the reference (paths relative to /root/reference):
+ *
+ *  rp_projector_create / _create_from_device / _export
+ *      R = srp.components_.T.astype(np.float32)          code/clustermode/randomProjection.py:101
+ *      sc.broadcast(R)                                   code/clustermode/randomProjection.py:104
+ *      (closure capture in localmode)                    code/localmode/randomProjection.py:127,130
+ *      other = self.__class__(other)  # CSC->CSR per call  scipy/sparse/_compressed.py:564
+ *    R is uploaded once, in a single-magnitude packed layout when it qualifies (every sklearn SRP
+ *    matrix does), and stays resident in HBM; _export/_create_from_device let a driver ship the
+ *    device image to other GPUs over RCCL (one broadcast) instead of re-packing.
+ *
+ *  rp_project_device
+ *      projected_features = features_matrix.dot(local_csr_matrix)
+ *                                                        code/clustermode/randomProjection.py:46
+ *      -> scipy _sparsetools.csr_matmat_maxnnz + csr_matmat  scipy/sparse/_compressed.py:569-595
+ *    Device-resident CSR in, device-resident CSR out, one kernel launch (single pass: count, scan
+ *    via decoupled look-back, fill). Output equals scipy's bit for bit: same per-row order
+ *    (RP_ORDER_SCIPY = reverse first-touch) or ascending (RP_ORDER_SORTED = what pyspark's
+ *    SparseVector makes of it, code/clustermode/randomProjection.py:49-50), same zero drop, values
+ *    computed with the same separately rounded multiply and add.
+ *
+ *  rp_project_host_begin / rp_result_fetch / rp_result_free
+ *      the same product for host buffers, shaped like scipy's two calls: begin computes C on the
+ *      GPU and reports its exact nnz (the role of csr_matmat_maxnnz: size the output), the caller
+ *      allocates, fetch fills (the role of csr_matmat). Used by the Python drop-ins
+ *      random_project_mappartitions_function (clustermode/randomProjection.py:15-54),
+ *      random_project_map_function (localmode/randomProjection.py:15-36) and
+ *      SparseRandomProjection.transform (sklearn/random_projection.py:801-824).
+ *
+ *  rp_synth_rows_device
+ *      synthetic KDD2012-shaped rows generated in HBM (benchmarks; the reference downloads
+ *      kdd12.tr with code/get_kdd2012_data.sh, not available offline).
+ */
+#ifndef RP_H
+#define RP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    RP_OK = 0,
+    RP_ERR_INVALID = 1,      /* bad argument (shape mismatch, bad dtype code, NULL pointer) */
+    RP_ERR_HIP = 2,          /* a HIP runtime call failed (no device, launch failure, ...) */
+    RP_ERR_CAPACITY = 3,     /* rp_project_device: out->capacity < exact nnz (nnz reported) */
+    RP_ERR_UNSUPPORTED = 4,  /* shape outside what the GPU path supports (see rp_last_error) */
+    RP_ERR_NOMEM = 5,
+    RP_ERR_TIMEOUT = 6       /* a device-side bounded wait expired (should never happen) */
+} rp_status;
+
+typedef enum { RP_I32 = 1, RP_I64 = 2, RP_F32 = 3, RP_F64 = 4 } rp_dtype;
+
+typedef enum {
+    RP_LAYOUT_AUTO = 0,      /* packed when R has one magnitude and p <= 8192, else generic */
+    RP_LAYOUT_GENERIC = 1,   /* CSR (int32 indptr, uint16 columns, values) */
+    RP_LAYOUT_PACKED = 2     /* require the packed layout; RP_ERR_UNSUPPORTED if R does not fit */
+} rp_layout;
+
+typedef enum { RP_ORDER_SCIPY = 0, RP_ORDER_SORTED = 1 } rp_order;
+
+typedef struct rp_projector rp_projector;
+typedef struct rp_result rp_result;
+
+/* Static description of a resident R (for logging and for shipping the device image). */
+typedef struct {
+    int64_t m;               /* rows of R = input features */
+    int64_t p;               /* columns of R = output components */
+    int64_t nnz;
+    int32_t layout;          /* RP_LAYOUT_GENERIC or RP_LAYOUT_PACKED */
+    int32_t value_type;      /* RP_F32 / RP_F64: dtype R was given in */
+    double magnitude;        /* packed: |value| of every entry; generic: 0 */
+    int32_t block_shift;     /* packed: features per overflow block = 1 << block_shift */
+    int32_t n_buffers;       /* device buffers making up the image (<= 4) */
+    int64_t buffer_bytes[4]; /* packed: W(u16[m]), block base(u32), records(u16); generic: Bp, Bj, Bx */
+} rp_projector_info;
+
+/* A CSR operand. Host or device memory depending on the call. */
+typedef struct {
+    int64_t n_rows;
+    const void* indptr;      /* n_rows + 1 entries, RP_I32 or RP_I64, indptr[0] may be != 0 */
+    int32_t indptr_type;
+    const int32_t* indices;  /* int32 feature ids in [0, m) */
+    const void* data;        /* RP_F32 or RP_F64 = the compute type (scipy upcast of A and R) */
+    int32_t data_type;
+    int64_t nnz;             /* indptr[n_rows] - indptr[0] if known (sizes tiles), else -1: the
+                                device call then reads it back (one small synchronous copy) */
+} rp_csr_in;
+
+/* Device output of rp_project_device (caller-owned device memory). */
+typedef struct {
+    void* indptr;            /* n_rows + 1 entries */
+    int32_t indptr_type;     /* RP_I32 or RP_I64 */
+    void* indices;           /* capacity entries */
+    int32_t indices_type;    /* RP_I32 or RP_I64 */
+    void* data;              /* capacity entries of the compute type */
+    int64_t capacity;
+} rp_csr_out;
+
+const char* rp_last_error(void);
+const char* rp_version(void);
+int rp_device_count(int* count);
+
+int rp_projector_create(int device, int64_t m, int64_t p,
+                        const void* indptr, int32_t indptr_type,
+                        const void* indices, int32_t indices_type,
+                        const void* data, int32_t data_type,
+                        int32_t layout, rp_projector** out);
+int rp_projector_info_get(const rp_projector* h, rp_projector_info* out);
+/* copy device buffer `which` (< info.n_buffers) of the image into caller device memory dst */
+int rp_projector_export(const rp_projector* h, int32_t which, void* dst_device, void* stream);
+/* build a projector on `device` from an image already in device memory (e.g. after an RCCL
+ * broadcast); the buffers are copied, the caller keeps ownership of `buffers` */
+int rp_projector_create_from_device(int device, const rp_projector_info* info,
+                                    const void* const* buffers, rp_projector** out);
+int rp_projector_destroy(rp_projector* h);
+
+/* Workspace bytes rp_project_device needs for n_rows (look-back tile states + counters). */
+int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows);
+
+/* C = A @ R, all device memory, enqueued on `stream` (hipStream_t, NULL = default).
+ * workspace: caller device memory of rp_project_workspace_bytes(), or NULL to use the
+ * projector's own (then calls on one projector must not run concurrently on different streams).
+ * total_nnz: if non-NULL the call synchronizes the stream and stores the exact output nnz;
+ * RP_ERR_CAPACITY is returned when it exceeds out->capacity (indptr is still complete).
+ * If NULL the call is fully asynchronous (timing loops, graph capture). */
+int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int32_t order,
+                      void* workspace, void* stream, int64_t* total_nnz);
+
+/* Host CSR in -> GPU -> exact nnz. The result stays on the device until fetched. */
+int rp_project_host_begin(rp_projector* h, const rp_csr_in* a_host, int32_t order,
+                          rp_result** out, int64_t* nnz);
+/* Copy into caller host arrays: indptr (n_rows + 1) of indptr_type, indices (nnz) of
+ * indices_type, data (nnz) of the compute type. */
+int rp_result_fetch(rp_result* r, void* indptr, int32_t indptr_type, void* indices,
+                    int32_t indices_type, void* data);
+int rp_result_free(rp_result* r);
+
+/* Synthetic rows on the device: per-row nnz = 1 + Poisson(mean_extra) (capped at max_row_nnz),
+ * distinct ascending columns in [0, m) — uniform (dist 0) or power-law Zipf(s) over a fixed
+ * permutation without replacement (dist 1) — values 1.0f. Two calls: first with indices == NULL
+ * to fill indptr (int32 or int64) and get the nnz, then with indices/data of that size. */
+int rp_synth_rows_device(int device, int64_t n_rows, int64_t m, double mean_extra,
+                         int32_t max_row_nnz, int32_t dist, double zipf_s, uint64_t seed,
+                         void* indptr, int32_t indptr_type, int32_t* indices, float* data,
+                         void* stream, int64_t* nnz);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RP_H */

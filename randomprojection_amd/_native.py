@@ -1,0 +1,134 @@
+"""ctypes binding of librp.so (include/rp.h). The product has no CPU fallback: if the library or a
+GPU is missing, every compute call raises ``NativeUnavailable``/``RPError`` loudly."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librp.so")
+
+RP_OK, RP_ERR_INVALID, RP_ERR_HIP, RP_ERR_CAPACITY, RP_ERR_UNSUPPORTED, RP_ERR_NOMEM, RP_ERR_TIMEOUT = range(7)
+RP_I32, RP_I64, RP_F32, RP_F64 = 1, 2, 3, 4
+RP_LAYOUT_AUTO, RP_LAYOUT_GENERIC, RP_LAYOUT_PACKED = 0, 1, 2
+RP_ORDER_SCIPY, RP_ORDER_SORTED = 0, 1
+
+# every symbol include/rp.h declares (tests/test_abi.py checks the .so exports them all)
+EXPORTS = (
+    "rp_last_error", "rp_version", "rp_device_count",
+    "rp_projector_create", "rp_projector_info_get", "rp_projector_export",
+    "rp_projector_create_from_device", "rp_projector_destroy",
+    "rp_project_workspace_bytes", "rp_project_device",
+    "rp_project_host_begin", "rp_result_fetch", "rp_result_free",
+    "rp_synth_rows_device",
+)
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class RPError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"librp error {code}: {msg}")
+        self.code = code
+
+
+class ProjectorInfo(ctypes.Structure):
+    _fields_ = [
+        ("m", ctypes.c_int64), ("p", ctypes.c_int64), ("nnz", ctypes.c_int64),
+        ("layout", ctypes.c_int32), ("value_type", ctypes.c_int32),
+        ("magnitude", ctypes.c_double), ("block_shift", ctypes.c_int32),
+        ("n_buffers", ctypes.c_int32), ("buffer_bytes", ctypes.c_int64 * 4),
+    ]
+
+
+class CsrIn(ctypes.Structure):
+    _fields_ = [
+        ("n_rows", ctypes.c_int64), ("indptr", ctypes.c_void_p), ("indptr_type", ctypes.c_int32),
+        ("indices", ctypes.c_void_p), ("data", ctypes.c_void_p), ("data_type", ctypes.c_int32),
+        ("nnz", ctypes.c_int64),
+    ]
+
+
+class CsrOut(ctypes.Structure):
+    _fields_ = [
+        ("indptr", ctypes.c_void_p), ("indptr_type", ctypes.c_int32),
+        ("indices", ctypes.c_void_p), ("indices_type", ctypes.c_int32),
+        ("data", ctypes.c_void_p), ("capacity", ctypes.c_int64),
+    ]
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load librp.so (built by ``randomprojection_amd.build`` / ``__graft_entry__.build``)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise NativeUnavailable(
+            f"{path} is missing: build it with `python -m randomprojection_amd.build` "
+            "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    lib = ctypes.CDLL(path)
+    vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    P = ctypes.POINTER
+    sig = {
+        "rp_last_error": (ctypes.c_char_p, []),
+        "rp_version": (ctypes.c_char_p, []),
+        "rp_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
+        "rp_projector_create": (ctypes.c_int, [ctypes.c_int, i64, i64, vp, i32, vp, i32, vp, i32, i32, P(vp)]),
+        "rp_projector_info_get": (ctypes.c_int, [vp, P(ProjectorInfo)]),
+        "rp_projector_export": (ctypes.c_int, [vp, i32, vp, vp]),
+        "rp_projector_create_from_device": (ctypes.c_int, [ctypes.c_int, P(ProjectorInfo), P(vp), P(vp)]),
+        "rp_projector_destroy": (ctypes.c_int, [vp]),
+        "rp_project_workspace_bytes": (i64, [vp, i64]),
+        "rp_project_device": (ctypes.c_int, [vp, P(CsrIn), P(CsrOut), i32, vp, vp, P(i64)]),
+        "rp_project_host_begin": (ctypes.c_int, [vp, P(CsrIn), i32, P(vp), P(i64)]),
+        "rp_result_fetch": (ctypes.c_int, [vp, vp, i32, vp, i32, vp]),
+        "rp_result_free": (ctypes.c_int, [vp]),
+        "rp_synth_rows_device": (ctypes.c_int, [ctypes.c_int, i64, i64, dbl, i32, i32, dbl, ctypes.c_uint64,
+                                                vp, i32, vp, vp, vp, P(i64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != RP_OK:
+        raise RPError(rc, load().rp_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = load().rp_device_count(ctypes.byref(n))
+    return n.value if rc == RP_OK else 0
+
+
+def idx_code(dtype) -> int:
+    dtype = np.dtype(dtype)
+    if dtype == np.int32:
+        return RP_I32
+    if dtype == np.int64:
+        return RP_I64
+    raise TypeError(f"index dtype must be int32 or int64, got {dtype}")
+
+
+def val_code(dtype) -> int:
+    dtype = np.dtype(dtype)
+    if dtype == np.float32:
+        return RP_F32
+    if dtype == np.float64:
+        return RP_F64
+    raise TypeError(f"value dtype must be float32 or float64, got {dtype}")
+
+
+def ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data) if a.size else ctypes.c_void_p(a.ctypes.data or 0)

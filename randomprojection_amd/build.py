@@ -1,0 +1,38 @@
+"""Build librp.so (HIP, gfx950) in-tree with hipcc. No CUDA, no hipify, no multi-target build."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = [os.path.join(HERE, "csrc", "rp_spgemm.hip")]
+OUT = os.path.join(HERE, "librp.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = [
+    "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+    # scipy's csr_matmat rounds the multiply and the add separately: never contract to FMA
+    "-ffp-contract=off", "-fno-fast-math", "-Wall",
+]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    deps = SRC + [os.path.join(HERE, "..", "include", "rp.h")]
+    return any(os.path.getmtime(s) > t for s in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if force or needs_build():
+        cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *SRC]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,1314 @@
+// rp_spgemm.hip — MI355X (gfx950) projection step C = A @ R of afcarl/RandomProjection.
+//
+// Reference path (paths relative to /root/reference):
+//   code/clustermode/randomProjection.py:46  projected_features = features_matrix.dot(local_csr_matrix)
+//   -> scipy/sparse/_compressed.py:546-604 _matmul_sparse -> _sparsetools csr_matmat_maxnnz + csr_matmat
+// Semantics reproduced bit for bit: for every A row, products Ax[jj]*Bx[kk] in
+// (jj, kk) storage order, each multiply rounded, then added into sums[k] (starting at +0); output
+// entries = distinct touched k with sums[k] != 0, in reverse first-touch order (or ascending).
+//
+// Design: one launch, one workgroup per tile of up to 256 rows, tiles taken in
+// dispatch order from an atomic counter, and a single-pass decoupled look-back over tile nnz so
+// the output is written exactly once at its final CSR position:
+//   stage 1  (flat over the tile's A entries, coalesced): gather each feature's R row descriptor
+//            (packed: one u16 word per feature, L2/MALL resident) and scan product counts in LDS;
+//            write every product x*b (rounded once) into an LDS product array, grouped by row.
+//   stage 2  (one lane per row): walk the row's products in order, accumulating into a list kept
+//            in place at the front of the row's own product slots; count nonzero sums.
+//   stage 3  block scan of row counts, look-back for the tile's global offset, rows' entries
+//            staged in LDS in final order, then written with coalesced stores.
+// Tiles whose entries/products exceed the LDS caps run a sequential exact path (scipy's dense
+// sums/next accumulator in LDS), so any input is handled.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rp.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// error plumbing
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(RP_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
+                        __FILE__, __LINE__);                                                   \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------
+// constants
+constexpr int kBlock = 256;          // threads per workgroup = max rows per tile
+constexpr int kMaxE = 16;            // strided A entries held per thread in stage 1
+constexpr int kCapAMax = kBlock * kMaxE;  // 4096 entries per tile at most on the fast path
+constexpr int kRowProdMax = 192;     // a row with more products goes to the exact dense path
+
+constexpr uint64_t kFlagA = 1ull << 62;   // tile aggregate published
+constexpr uint64_t kFlagP = 2ull << 62;   // tile inclusive prefix published
+constexpr uint64_t kValMask = (1ull << 62) - 1;
+constexpr long kSpinLimit = 1l << 27;     // bounded waits (with s_sleep): seconds, never minutes
+
+struct Workspace {              // device memory header; tile states follow at +64 bytes
+    unsigned int tile_counter;
+    unsigned int error;
+    unsigned long long total;
+    unsigned long long pad[6];
+};
+
+// ------------------------------------------------------------------------------------------
+// R layouts
+//
+// Packed (single magnitude, p <= 8192): one 16-bit word per feature j:
+//   0                         : no entries
+//   01 s ccccccccccccc        : one entry, sign s, column c (13 bits)
+//   1  ooooooooooooooo        : >= 2 entries, record at O[base[j >> bs] + o]:
+//                               O[rec] = count n, O[rec+1..rec+n] = (sign << 15) | column
+// Value of an entry = sign ? -mag : mag, so x * value == x * Bx bitwise (IEEE negation symmetry).
+struct PackedR {
+    const uint16_t* W;
+    const uint32_t* base;
+    const uint16_t* O;
+    int bs;
+};
+// Generic CSR (any values): Bp int32 (m + 1), Bj uint16, Bx in the compute type.
+template <typename T>
+struct GenericR {
+    const int32_t* Bp;
+    const uint16_t* Bj;
+    const T* Bx;
+};
+
+// descriptor of the R row of one A entry, produced in stage 1
+//   packed : d = single entry (bit 31 clear), or 0x80000000 | (record offset + 1) (first entry)
+//   generic: d = Bp[j]
+template <typename T>
+__device__ __forceinline__ uint32_t r_describe(const PackedR& R, int32_t j, uint32_t& cnt) {
+    uint32_t w = R.W[j];
+    if (w & 0x8000u) {
+        uint32_t rec = R.base[j >> R.bs] + (w & 0x7fffu);
+        cnt = R.O[rec];
+        return 0x80000000u | (rec + 1);
+    }
+    cnt = (w >> 14) & 1u;
+    return w & 0x3fffu;
+}
+template <typename T>
+__device__ __forceinline__ uint32_t r_describe(const GenericR<T>& R, int32_t j, uint32_t& cnt) {
+    int32_t b0 = R.Bp[j];
+    cnt = (uint32_t)(R.Bp[j + 1] - b0);
+    return (uint32_t)b0;
+}
+
+template <typename T>
+__device__ __forceinline__ T tmul(T a, T b);
+template <>
+__device__ __forceinline__ float tmul<float>(float a, float b) { return __fmul_rn(a, b); }
+template <>
+__device__ __forceinline__ double tmul<double>(double a, double b) { return __dmul_rn(a, b); }
+template <typename T>
+__device__ __forceinline__ T tadd(T a, T b);
+template <>
+__device__ __forceinline__ float tadd<float>(float a, float b) { return __fadd_rn(a, b); }
+template <>
+__device__ __forceinline__ double tadd<double>(double a, double b) { return __dadd_rn(a, b); }
+
+// t-th product (column, x * value) of an entry described by d
+template <typename T>
+__device__ __forceinline__ void r_product(const PackedR& R, T mag, uint32_t d, uint32_t t, T x,
+                                          uint32_t& col, T& v) {
+    uint32_t e;
+    if (d & 0x80000000u) {
+        e = R.O[(d & 0x7fffffffu) + t];
+        col = e & 0x7fffu;
+        v = tmul<T>(x, (e & 0x8000u) ? -mag : mag);
+    } else {
+        col = d & 0x1fffu;
+        v = tmul<T>(x, (d & 0x2000u) ? -mag : mag);
+    }
+}
+template <typename T>
+__device__ __forceinline__ void r_product(const GenericR<T>& R, T, uint32_t d, uint32_t t, T x,
+                                          uint32_t& col, T& v) {
+    col = R.Bj[d + t];
+    v = tmul<T>(x, R.Bx[d + t]);
+}
+
+// ------------------------------------------------------------------------------------------
+// block-level helpers (256 threads = 4 waves of 64)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// exclusive scan of one value per thread; *total = block sum. Contains two barriers.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wsum, uint32_t* total) {
+    const uint32_t inc = wave_incl_scan(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) s_wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < kBlock / 64; ++i) {
+        uint32_t s = s_wsum[i];
+        base += (i < w) ? s : 0u;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - v;
+}
+
+// decoupled look-back (thread 0 only): publish this tile's aggregate, sum predecessors' aggregates
+// until an inclusive prefix is found, publish the inclusive prefix. Each state is one 8-byte
+// granule {flag, value} written and read with relaxed agent-scope atomics (sc1), so no separate
+// payload needs ordering (MI355X_MICROARCH.md, Workgroup dispatch: granule hand-off).
+__device__ unsigned long long lookback(unsigned long long* states, unsigned int tile,
+                                       unsigned long long agg, Workspace* ws) {
+    if (tile == 0) {
+        __hip_atomic_store(&states[0], kFlagP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0;
+    }
+    __hip_atomic_store(&states[tile], kFlagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long excl = 0;
+    long i = (long)tile - 1;
+    long spins = 0;
+    while (i >= 0) {
+        unsigned long long s =
+            __hip_atomic_load(&states[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s == 0) {
+            if (++spins > kSpinLimit) {
+                atomicOr(&ws->error, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += s & kValMask;
+        if ((s & ~kValMask) == kFlagP) break;
+        --i;
+    }
+    __hip_atomic_store(&states[tile], kFlagP | (excl + agg), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
+// ------------------------------------------------------------------------------------------
+// exact sequential path for tiles beyond the LDS caps: scipy's dense sums/next accumulator in
+// LDS, one lane. Pass 0 counts, pass 1 writes (after the look-back gave the tile offset).
+template <typename T, typename IP, typename OP, typename OI, typename RL>
+__device__ void heavy_tile(const RL& R, T mag, const IP* __restrict__ Ap,
+                           const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t row0,
+                           int nrows, int p, unsigned char* lds, uint32_t* s_rowc, int pass,
+                           unsigned long long tile_off, OP* __restrict__ Cp,
+                           OI* __restrict__ Cj, T* __restrict__ Cx, bool write_entries,
+                           int order) {
+    T* sums = reinterpret_cast<T*>(lds);
+    int16_t* next = reinterpret_cast<int16_t*>(lds + sizeof(T) * (size_t)p);
+    for (int k = threadIdx.x; k < p; k += kBlock) {
+        sums[k] = T(0);
+        next[k] = -1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long off = tile_off;
+        for (int r = 0; r < nrows; ++r) {
+            int head = -2, length = 0;
+            const int64_t jb = (int64_t)Ap[row0 + r], je = (int64_t)Ap[row0 + r + 1];
+            for (int64_t jj = jb; jj < je; ++jj) {
+                const int32_t j = Aj[jj];
+                const T x = Ax[jj];
+                uint32_t cnt;
+                const uint32_t d = r_describe<T>(R, j, cnt);
+                for (uint32_t t = 0; t < cnt; ++t) {
+                    uint32_t k;
+                    T v;
+                    r_product<T>(R, mag, d, t, x, k, v);
+                    sums[k] = tadd<T>(sums[k], v);
+                    if (next[k] == -1) {
+                        next[k] = (int16_t)head;
+                        head = (int)k;
+                        ++length;
+                    }
+                }
+            }
+            uint32_t c = 0;
+            const unsigned long long row_off = off;
+            for (int q = 0; q < length; ++q) {
+                const T s = sums[head];
+                if (s != T(0)) {
+                    if (pass == 1 && write_entries) {
+                        Cj[off] = (OI)head;
+                        Cx[off] = s;
+                    }
+                    ++off;
+                    ++c;
+                }
+                const int tmp = head;
+                head = next[head];
+                next[tmp] = -1;
+                sums[tmp] = T(0);
+            }
+            if (pass == 0) {
+                s_rowc[r] = c;
+            } else {
+                Cp[row0 + r] = (OP)row_off;
+                if (order == RP_ORDER_SORTED && write_entries && c > 1) {
+                    // shell sort of the row segment by column (rare path)
+                    const unsigned long long n = c;
+                    for (unsigned long long gap = n / 2; gap > 0; gap /= 2)
+                        for (unsigned long long a = gap; a < n; ++a) {
+                            OI kc = Cj[row_off + a];
+                            T kv = Cx[row_off + a];
+                            unsigned long long b = a;
+                            while (b >= gap && Cj[row_off + b - gap] > kc) {
+                                Cj[row_off + b] = Cj[row_off + b - gap];
+                                Cx[row_off + b] = Cx[row_off + b - gap];
+                                b -= gap;
+                            }
+                            Cj[row_off + b] = kc;
+                            Cx[row_off + b] = kv;
+                        }
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------
+// the fused kernel
+struct Caps {
+    int cap_a;   // A entries per tile on the fast path (<= kCapAMax)
+    int cap_p;   // products per tile on the fast path
+    int rpt;     // rows per tile (<= kBlock)
+};
+
+template <typename T, typename IP, typename OP, typename OI, typename RL>
+__global__ void __launch_bounds__(kBlock)
+spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict__ Ap,
+                       const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
+                       OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
+                       unsigned long long capacity, Caps caps, int order, Workspace* ws,
+                       unsigned int n_tiles) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    __shared__ uint32_t s_rowptr[kBlock + 1];
+    __shared__ uint32_t s_rowc[kBlock];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    __shared__ unsigned int s_tile;
+    __shared__ int s_heavy;
+    __shared__ unsigned long long s_off;
+
+    unsigned long long* states = reinterpret_cast<unsigned long long*>(ws + 1);
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        s_tile = atomicAdd(&ws->tile_counter, 1u);
+        s_heavy = 0;
+    }
+    __syncthreads();
+    const unsigned int tile = s_tile;
+    if (tile >= n_tiles) return;  // uniform
+
+    const int64_t row0 = (int64_t)tile * caps.rpt;
+    const int nrows = (int)std::min<int64_t>(caps.rpt, n_rows - row0);
+    const int64_t ea = (int64_t)Ap[row0];
+    const int64_t eb = (int64_t)Ap[row0 + nrows];
+    const int64_t nnz_t = eb - ea;
+
+    // LDS carve-up of the dynamic region:
+    //   X: eoff[cap_a + 1] (u32)  | later: staged output cols (u16) + vals (T)
+    //   P: pk[cap_p] (u16), pv[cap_p] (T)
+    const size_t x_bytes = std::max<size_t>(sizeof(uint32_t) * (caps.cap_a + 1),
+                                            (sizeof(uint16_t) + sizeof(T)) * caps.cap_p + 16);
+    const size_t x_bytes_al = (x_bytes + 15) & ~size_t(15);
+    uint32_t* s_eoff = reinterpret_cast<uint32_t*>(lds);
+    T* s_ov = reinterpret_cast<T*>(lds);  // staged values (8-aligned start)
+    uint16_t* s_oc = reinterpret_cast<uint16_t*>(lds + sizeof(T) * caps.cap_p);
+    T* s_pv = reinterpret_cast<T*>(lds + x_bytes_al);
+    uint16_t* s_pk = reinterpret_cast<uint16_t*>(lds + x_bytes_al + sizeof(T) * caps.cap_p);
+
+    bool heavy = nnz_t > caps.cap_a;  // uniform
+    uint32_t d[kMaxE];
+    T x[kMaxE];
+    uint32_t P_t = 0;
+    if (!heavy) {
+        const uint32_t ne = (uint32_t)nnz_t;
+        for (int r = tid; r <= nrows; r += kBlock) s_rowptr[r] = (uint32_t)((int64_t)Ap[row0 + r] - ea);
+        // stage 1a: gather R row descriptors, counts into eoff
+#pragma unroll
+        for (int i = 0; i < kMaxE; ++i) {
+            const uint32_t e = tid + i * kBlock;
+            d[i] = 0;
+            x[i] = T(0);
+            if (e < ne) {
+                const int32_t j = Aj[ea + e];
+                x[i] = Ax[ea + e];
+                uint32_t cnt;
+                d[i] = r_describe<T>(R, j, cnt);
+                s_eoff[e] = cnt;
+            }
+        }
+        __syncthreads();
+        // stage 1b: exclusive scan of counts (contiguous chunk per thread)
+        const uint32_t per = (ne + kBlock - 1) / kBlock;
+        const uint32_t c0 = std::min<uint32_t>(tid * per, ne), c1 = std::min<uint32_t>(c0 + per, ne);
+        uint32_t local = 0;
+        for (uint32_t e = c0; e < c1; ++e) local += s_eoff[e];
+        uint32_t total;
+        uint32_t run = block_excl_scan(local, s_wsum, &total);
+        for (uint32_t e = c0; e < c1; ++e) {
+            const uint32_t c = s_eoff[e];
+            s_eoff[e] = run;
+            run += c;
+        }
+        if (tid == 0) s_eoff[ne] = total;
+        P_t = total;
+        __syncthreads();
+        heavy = P_t > (uint32_t)caps.cap_p;  // uniform
+        if (!heavy) {
+            // stage 1c: products into LDS, in (entry, R-entry) order
+#pragma unroll
+            for (int i = 0; i < kMaxE; ++i) {
+                const uint32_t e = tid + i * kBlock;
+                if (e < ne) {
+                    const uint32_t o0 = s_eoff[e], o1 = s_eoff[e + 1];
+                    for (uint32_t t = 0; t < o1 - o0; ++t) {
+                        uint32_t col;
+                        T v;
+                        r_product<T>(R, mag, d[i], t, x[i], col, v);
+                        s_pk[o0 + t] = (uint16_t)col;
+                        s_pv[o0 + t] = v;
+                    }
+                }
+            }
+            __syncthreads();
+            // stage 2: per-row ordered accumulation, list in place at the front of the row's slots
+            uint32_t c = 0, n = 0, s = 0;
+            if (tid < nrows) {
+                s = s_eoff[s_rowptr[tid]];
+                const uint32_t t_end = s_eoff[s_rowptr[tid + 1]];
+                if (t_end - s > (uint32_t)kRowProdMax) {
+                    s_heavy = 1;
+                } else {
+                    for (uint32_t q = s; q < t_end; ++q) {
+                        const uint16_t k = s_pk[q];
+                        const T v = s_pv[q];
+                        uint32_t f = 0;
+                        while (f < n && s_pk[s + f] != k) ++f;
+                        if (f < n) {
+                            s_pv[s + f] = tadd<T>(s_pv[s + f], v);
+                        } else {
+                            s_pk[s + n] = k;
+                            s_pv[s + n] = tadd<T>(T(0), v);
+                            ++n;
+                        }
+                    }
+                    for (uint32_t f = 0; f < n; ++f) c += (s_pv[s + f] != T(0)) ? 1u : 0u;
+                }
+            }
+            __syncthreads();
+            if (!s_heavy) {
+                // stage 3: tile offsets, look-back, staged coalesced write
+                uint32_t tile_c;
+                const uint32_t o_r = block_excl_scan(tid < nrows ? c : 0u, s_wsum, &tile_c);
+                if (tid == 0) s_off = lookback(states, tile, tile_c, ws);
+                __syncthreads();
+                const unsigned long long G = s_off;
+                const bool write = G + tile_c <= capacity;
+                if (tid < nrows) {
+                    Cp[row0 + tid] = (OP)(G + o_r);
+                    if (order == RP_ORDER_SORTED) {
+                        // insertion sort of the row's list by column (lists are short)
+                        for (uint32_t a = 1; a < n; ++a) {
+                            const uint16_t kc = s_pk[s + a];
+                            const T kv = s_pv[s + a];
+                            uint32_t b = a;
+                            while (b > 0 && s_pk[s + b - 1] > kc) {
+                                s_pk[s + b] = s_pk[s + b - 1];
+                                s_pv[s + b] = s_pv[s + b - 1];
+                                --b;
+                            }
+                            s_pk[s + b] = kc;
+                            s_pv[s + b] = kv;
+                        }
+                        uint32_t w = o_r;
+                        for (uint32_t f = 0; f < n; ++f) {
+                            const T v = s_pv[s + f];
+                            if (v != T(0)) {
+                                s_oc[w] = s_pk[s + f];
+                                s_ov[w] = v;
+                                ++w;
+                            }
+                        }
+                    } else {
+                        uint32_t w = o_r;
+                        for (uint32_t f = n; f-- > 0;) {  // reverse first-touch order
+                            const T v = s_pv[s + f];
+                            if (v != T(0)) {
+                                s_oc[w] = s_pk[s + f];
+                                s_ov[w] = v;
+                                ++w;
+                            }
+                        }
+                    }
+                }
+                if (tile == n_tiles - 1 && tid == 0) {
+                    Cp[n_rows] = (OP)(G + tile_c);
+                    ws->total = G + tile_c;
+                }
+                __syncthreads();
+                if (write) {
+                    for (uint32_t q = tid; q < tile_c; q += kBlock) {
+                        Cj[G + q] = (OI)s_oc[q];
+                        Cx[G + q] = s_ov[q];
+                    }
+                }
+                return;
+            }
+            heavy = true;
+        }
+    }
+    // ---- exact sequential path (uniform branch)
+    heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, 0, 0, Cp, Cj,
+                                  Cx, false, order);
+    uint32_t tile_c;
+    (void)block_excl_scan(tid < nrows ? s_rowc[tid] : 0u, s_wsum, &tile_c);
+    if (tid == 0) s_off = lookback(states, tile, tile_c, ws);
+    __syncthreads();
+    const unsigned long long G = s_off;
+    const bool write = G + tile_c <= capacity;
+    heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, 1, G, Cp, Cj,
+                                  Cx, write, order);
+    if (tile == n_tiles - 1 && tid == 0) {
+        Cp[n_rows] = (OP)(G + tile_c);
+        ws->total = G + tile_c;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// small helper kernels
+template <typename S, typename D>
+__global__ void convert_kernel(const S* __restrict__ s, D* __restrict__ d, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        d[i] = (D)s[i];
+}
+
+template <typename S, typename D>
+__global__ void rebase_kernel(const S* __restrict__ s, D* __restrict__ d, int64_t n, int64_t add) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        d[i] = (D)((int64_t)s[i] + add);
+}
+
+// ---- synthetic rows: counter-based RNG (splitmix64 of seed, row, draw)
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double u01(uint64_t h) { return ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0); }
+
+__device__ int synth_count(uint64_t seed, int64_t row, double lam, int cap) {
+    // 1 + Poisson(lam) by inversion
+    const double u = u01(mix64(seed ^ mix64((uint64_t)row * 2 + 1)));
+    double pk = exp(-lam), cdf = pk;
+    int k = 0;
+    while (u > cdf && k < 4096) {
+        ++k;
+        pk *= lam / k;
+        cdf += pk;
+    }
+    return std::min(1 + k, cap);
+}
+
+template <typename IP>
+__global__ void synth_count_kernel(int64_t n_rows, uint64_t seed, double lam, int cap, int64_t m,
+                                   IP* __restrict__ counts) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_rows;
+         i += (int64_t)gridDim.x * blockDim.x)
+        counts[i + 1] = (IP)std::min<int64_t>(synth_count(seed, i, lam, cap), m);
+}
+
+constexpr int kSynthMaxK = 256;
+
+__global__ void synth_fill_kernel(int64_t n_rows, int64_t m, uint64_t seed, int dist,
+                                  double zipf_s, uint64_t perm_a, uint64_t perm_b,
+                                  const int64_t* __restrict__ indptr, int32_t* __restrict__ Aj,
+                                  float* __restrict__ Ax) {
+    int32_t cols[kSynthMaxK];
+    const double one_minus_s = 1.0 - zipf_s;
+    const double top = pow((double)m + 1.0, one_minus_s);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_rows;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t b = indptr[i];
+        const int k = (int)(indptr[i + 1] - b);
+        uint64_t ctr = 0;
+        for (int t = 0; t < k; ++t) {
+            int32_t c;
+            bool dup;
+            do {
+                const uint64_t h = mix64(seed ^ mix64(((uint64_t)i << 20) ^ (ctr++) ^ 0xA5A5000000000000ull));
+                if (dist == 0) {
+                    c = (int32_t)(((h >> 32) * (uint64_t)m) >> 32);
+                } else {
+                    // bounded Zipf(s) rank by continuous inversion, then a fixed affine permutation
+                    const double u = u01(h);
+                    double xr = pow(1.0 - u * (1.0 - top), 1.0 / one_minus_s);
+                    int64_t rank = (int64_t)xr - 1;
+                    rank = rank < 0 ? 0 : (rank >= m ? m - 1 : rank);
+                    c = (int32_t)((perm_a * (uint64_t)rank + perm_b) % (uint64_t)m);
+                }
+                dup = false;
+                for (int q = 0; q < t; ++q) dup |= (cols[q] == c);
+            } while (dup);
+            // insertion into sorted position
+            int q = t;
+            while (q > 0 && cols[q - 1] > c) {
+                cols[q] = cols[q - 1];
+                --q;
+            }
+            cols[q] = c;
+        }
+        for (int t = 0; t < k; ++t) {
+            Aj[b + t] = cols[t];
+            Ax[b + t] = 1.0f;
+        }
+    }
+}
+
+// three-phase device scan (block sums, scan of block sums, add back) for int64 counts
+constexpr int kScanBlock = 1024;
+__global__ void scan_blocks_kernel(int64_t* a, int64_t n, int64_t* bsum) {
+    __shared__ int64_t s[kScanBlock];
+    const int64_t i = blockIdx.x * (int64_t)kScanBlock + threadIdx.x;
+    s[threadIdx.x] = i < n ? a[i] : 0;
+    __syncthreads();
+    for (int o = 1; o < kScanBlock; o <<= 1) {
+        int64_t t = threadIdx.x >= (unsigned)o ? s[threadIdx.x - o] : 0;
+        __syncthreads();
+        s[threadIdx.x] += t;
+        __syncthreads();
+    }
+    if (i < n) a[i] = s[threadIdx.x];
+    if (threadIdx.x == kScanBlock - 1) bsum[blockIdx.x] = s[threadIdx.x];
+}
+__global__ void scan_add_kernel(int64_t* a, int64_t n, const int64_t* bsum_scanned) {
+    const int64_t i = blockIdx.x * (int64_t)kScanBlock + threadIdx.x;
+    if (blockIdx.x > 0 && i < n) a[i] += bsum_scanned[blockIdx.x - 1];
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side structures
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int device = -1;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(device);
+            (void)hipFree(p);
+            (void)hipSetDevice(cur);
+        }
+        p = nullptr;
+        bytes = 0;
+    }
+    int ensure(size_t n, int dev) {
+        if (n <= bytes && p) return RP_OK;
+        release();
+        device = dev;
+        size_t want = std::max<size_t>(n, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(RP_ERR_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        }
+        bytes = want;
+        return RP_OK;
+    }
+};
+
+int inclusive_scan_i64(int64_t* a, int64_t n, hipStream_t st, DevBuf& tmp, int device) {
+    if (n <= 0) return RP_OK;
+    const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    int rc = tmp.ensure(sizeof(int64_t) * (size_t)(nb + 1), device);
+    if (rc) return rc;
+    int64_t* bs = (int64_t*)tmp.p;
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, a, n, bs);
+    if (nb > 1) {
+        DevBuf tmp2;
+        rc = inclusive_scan_i64(bs, nb, st, tmp2, device);
+        if (rc) return rc;
+        hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, a, n, bs);
+        HIP_TRY(hipStreamSynchronize(st));  // tmp2 freed at scope exit
+    }
+    HIP_TRY(hipGetLastError());
+    return RP_OK;
+}
+
+}  // namespace
+
+struct rp_projector {
+    int device = 0;
+    int64_t m = 0, p = 0, nnz = 0;
+    int layout = RP_LAYOUT_GENERIC;
+    int value_type = RP_F32;
+    double mag = 0.0;
+    int bs = 0;
+    // packed
+    DevBuf W, base, O;
+    // generic
+    DevBuf Bp, Bj, Bx32, Bx64;
+    // internal workspace and host-path staging
+    DevBuf ws;
+    DevBuf a_ptr, a_idx, a_val;
+    std::mutex mu;
+};
+
+struct rp_result {
+    rp_projector* h = nullptr;
+    int64_t n_rows = 0, nnz = 0;
+    int value_type = RP_F32;
+    DevBuf cp, cj, cx;  // int64 indptr, int32 indices, T data
+};
+
+namespace {
+
+int dtype_size(int t) {
+    switch (t) {
+        case RP_I32: case RP_F32: return 4;
+        case RP_I64: case RP_F64: return 8;
+        default: return 0;
+    }
+}
+
+template <typename I>
+int64_t idx_at(const void* a, int64_t i) { return (int64_t)((const I*)a)[i]; }
+int64_t ptr_at(const void* a, int t, int64_t i) {
+    return t == RP_I64 ? idx_at<int64_t>(a, i) : idx_at<int32_t>(a, i);
+}
+double val_at(const void* a, int t, int64_t i) {
+    return t == RP_F64 ? ((const double*)a)[i] : (double)((const float*)a)[i];
+}
+
+Caps choose_caps(int64_t n_rows, int64_t nnz_a, double prod_per_entry) {
+    Caps c;
+    c.cap_a = kCapAMax;
+    const double avg = n_rows > 0 ? (double)nnz_a / (double)n_rows : 1.0;
+    int rpt = kBlock;
+    const double want = 0.70 * c.cap_a / std::max(avg, 1e-9);
+    if (want < rpt) rpt = std::max(1, (int)want);
+    c.rpt = rpt;
+    const double prods = std::max(1.0, avg * rpt * prod_per_entry);
+    int cp = (int)std::min<double>(c.cap_a, std::max(1024.0, 1.6 * prods + 256.0));
+    c.cap_p = (cp + 63) & ~63;
+    return c;
+}
+
+size_t lds_bytes_for(const Caps& c, int value_size, int64_t p) {
+    const size_t x = std::max<size_t>(4u * (c.cap_a + 1), (size_t)(2 + value_size) * c.cap_p + 16);
+    const size_t xa = (x + 15) & ~size_t(15);
+    const size_t fast = xa + (size_t)(2 + value_size) * c.cap_p;
+    const size_t heavy = (size_t)(value_size + 2) * (size_t)p;
+    return std::max(fast, heavy);
+}
+
+template <typename T, typename IP, typename OP, typename OI, typename RL>
+int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
+                 int order, Workspace* ws, unsigned n_tiles, const Caps& caps, size_t lds,
+                 hipStream_t st) {
+    HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL>), dim3(n_tiles), dim3(kBlock), lds, st, R, mag, (int)h->p, a->n_rows,
+                       (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
+                       (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, caps, order,
+                       ws, n_tiles);
+    HIP_TRY(hipGetLastError());
+    return RP_OK;
+}
+
+template <typename T, typename RL>
+int dispatch_idx(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
+                 int order, Workspace* ws, unsigned n_tiles, const Caps& caps, size_t lds,
+                 hipStream_t st) {
+    const bool ip64 = a->indptr_type == RP_I64, op64 = c->indptr_type == RP_I64,
+               oi64 = c->indices_type == RP_I64;
+#define RP_L(IP, OP, OI) return launch_typed<T, IP, OP, OI, RL>(R, mag, h, a, c, order, ws, n_tiles, caps, lds, st)
+    if (!ip64 && !op64 && !oi64) RP_L(int32_t, int32_t, int32_t);
+    if (!ip64 && op64 && !oi64) RP_L(int32_t, int64_t, int32_t);
+    if (!ip64 && op64 && oi64) RP_L(int32_t, int64_t, int64_t);
+    if (ip64 && !op64 && !oi64) RP_L(int64_t, int32_t, int32_t);
+    if (ip64 && op64 && !oi64) RP_L(int64_t, int64_t, int32_t);
+    if (ip64 && op64 && oi64) RP_L(int64_t, int64_t, int64_t);
+    if (!ip64 && !op64 && oi64) RP_L(int32_t, int32_t, int64_t);
+    RP_L(int64_t, int32_t, int64_t);
+#undef RP_L
+}
+
+int ensure_generic_values(rp_projector* h, int T) {
+    if (h->layout != RP_LAYOUT_GENERIC) return RP_OK;
+    if (T == RP_F32) {
+        if (!h->Bx32.p) return fail(RP_ERR_INVALID, "R was given as float64; compute type float32 would round R (use float64)");
+        return RP_OK;
+    }
+    if (h->Bx64.p) return RP_OK;
+    int rc = h->Bx64.ensure(sizeof(double) * (size_t)std::max<int64_t>(h->nnz, 1), h->device);
+    if (rc) return rc;
+    if (h->nnz > 0) {
+        hipLaunchKernelGGL((convert_kernel<float, double>), dim3(1024), dim3(256), 0, nullptr,
+                           (const float*)h->Bx32.p, (double*)h->Bx64.p, h->nnz);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    return RP_OK;
+}
+
+int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
+                        void* workspace, hipStream_t st, int64_t* total_nnz, int64_t nnz_a_hint) {
+    if (!a || !c) return fail(RP_ERR_INVALID, "NULL operand");
+    if (a->n_rows < 0) return fail(RP_ERR_INVALID, "n_rows < 0");
+    if (a->data_type != RP_F32 && a->data_type != RP_F64)
+        return fail(RP_ERR_INVALID, "A data type must be RP_F32 or RP_F64");
+    if ((a->indptr_type != RP_I32 && a->indptr_type != RP_I64) ||
+        (c->indptr_type != RP_I32 && c->indptr_type != RP_I64) ||
+        (c->indices_type != RP_I32 && c->indices_type != RP_I64))
+        return fail(RP_ERR_INVALID, "index types must be RP_I32 or RP_I64");
+    if (a->data_type == RP_F32 && h->value_type == RP_F64)
+        return fail(RP_ERR_INVALID, "compute type must be upcast(A, R) = float64 for a float64 R");
+    if (a->n_rows >= (int64_t)1 << 40) return fail(RP_ERR_UNSUPPORTED, "too many rows");
+    int rc = ensure_generic_values(h, a->data_type);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(h->device));
+
+    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    const Caps caps = choose_caps(a->n_rows, nnz_a_hint >= 0 ? nnz_a_hint : a->n_rows * 11, ppe);
+    const size_t lds = lds_bytes_for(caps, dtype_size(a->data_type), h->p);
+    if (lds > 160 * 1024 - 4096)
+        return fail(RP_ERR_UNSUPPORTED, "p=%lld too large for the LDS accumulator (%zu bytes)",
+                    (long long)h->p, lds);
+    const int64_t n_tiles64 = a->n_rows > 0 ? (a->n_rows + caps.rpt - 1) / caps.rpt : 0;
+    if (n_tiles64 >= (int64_t)1 << 31) return fail(RP_ERR_UNSUPPORTED, "too many tiles");
+    const unsigned n_tiles = (unsigned)n_tiles64;
+    const size_t ws_bytes = sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(n_tiles64, 1);
+    Workspace* ws = (Workspace*)workspace;
+    if (!ws) {
+        rc = h->ws.ensure(ws_bytes, h->device);
+        if (rc) return rc;
+        ws = (Workspace*)h->ws.p;
+    }
+    HIP_TRY(hipMemsetAsync(ws, 0, ws_bytes, st));
+    if (n_tiles == 0) {
+        // empty A: indptr = [0]
+        if (c->indptr_type == RP_I64) {
+            int64_t z = 0;
+            HIP_TRY(hipMemcpyAsync(c->indptr, &z, 8, hipMemcpyHostToDevice, st));
+        } else {
+            int32_t z = 0;
+            HIP_TRY(hipMemcpyAsync(c->indptr, &z, 4, hipMemcpyHostToDevice, st));
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        if (total_nnz) *total_nnz = 0;
+        return RP_OK;
+    }
+    if (h->layout == RP_LAYOUT_PACKED) {
+        PackedR R{(const uint16_t*)h->W.p, (const uint32_t*)h->base.p, (const uint16_t*)h->O.p, h->bs};
+        rc = a->data_type == RP_F64
+                 ? dispatch_idx<double, PackedR>(R, h->mag, h, a, c, order, ws, n_tiles, caps, lds, st)
+                 : dispatch_idx<float, PackedR>(R, (float)h->mag, h, a, c, order, ws, n_tiles, caps, lds, st);
+    } else if (a->data_type == RP_F64) {
+        GenericR<double> R{(const int32_t*)h->Bp.p, (const uint16_t*)h->Bj.p, (const double*)h->Bx64.p};
+        rc = dispatch_idx<double, GenericR<double>>(R, 0.0, h, a, c, order, ws, n_tiles, caps, lds, st);
+    } else {
+        GenericR<float> R{(const int32_t*)h->Bp.p, (const uint16_t*)h->Bj.p, (const float*)h->Bx32.p};
+        rc = dispatch_idx<float, GenericR<float>>(R, 0.0f, h, a, c, order, ws, n_tiles, caps, lds, st);
+    }
+    if (rc) return rc;
+    if (total_nnz) {
+        Workspace hw;
+        HIP_TRY(hipMemcpyAsync(&hw, ws, sizeof hw, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (hw.error) return fail(RP_ERR_TIMEOUT, "device look-back wait expired");
+        *total_nnz = (int64_t)hw.total;
+        if ((int64_t)hw.total > c->capacity)
+            return fail(RP_ERR_CAPACITY, "output capacity %lld < nnz %lld", (long long)c->capacity,
+                        (long long)hw.total);
+    }
+    return RP_OK;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C-ABI
+extern "C" {
+
+const char* rp_last_error(void) { return g_err.c_str(); }
+const char* rp_version(void) { return "rp-mi355x 0.1 (gfx950)"; }
+
+int rp_device_count(int* count) {
+    if (!count) return fail(RP_ERR_INVALID, "NULL count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(RP_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = n;
+    return RP_OK;
+}
+
+int rp_projector_create(int device, int64_t m, int64_t p, const void* indptr, int32_t indptr_type,
+                        const void* indices, int32_t indices_type, const void* data,
+                        int32_t data_type, int32_t layout, rp_projector** out) {
+    if (!out) return fail(RP_ERR_INVALID, "NULL out");
+    *out = nullptr;
+    if (m < 0 || p <= 0) return fail(RP_ERR_INVALID, "bad shape (%lld, %lld)", (long long)m, (long long)p);
+    if (!indptr || (indptr_type != RP_I32 && indptr_type != RP_I64) ||
+        (indices_type != RP_I32 && indices_type != RP_I64) ||
+        (data_type != RP_F32 && data_type != RP_F64))
+        return fail(RP_ERR_INVALID, "bad R arrays");
+    if (p > 32767) return fail(RP_ERR_UNSUPPORTED, "p=%lld > 32767 not supported by the GPU path", (long long)p);
+    const int64_t nnz = ptr_at(indptr, indptr_type, m) - ptr_at(indptr, indptr_type, 0);
+    const int64_t b0 = ptr_at(indptr, indptr_type, 0);
+    if (nnz < 0 || nnz >= ((int64_t)1 << 31) - 1) return fail(RP_ERR_UNSUPPORTED, "R nnz out of range");
+    if (nnz > 0 && (!indices || !data)) return fail(RP_ERR_INVALID, "NULL R indices/data");
+    if (m >= ((int64_t)1 << 31)) return fail(RP_ERR_UNSUPPORTED, "m >= 2^31");
+
+    // validate and detect the single-magnitude layout
+    double mag = 0.0;
+    bool single = p <= 8192 && nnz > 0;
+    for (int64_t q = 0; q < nnz; ++q) {
+        const int64_t col = ptr_at(indices, indices_type, b0 + q);
+        if (col < 0 || col >= p) return fail(RP_ERR_INVALID, "R column index %lld out of range", (long long)col);
+        if (single) {
+            const double v = val_at(data, data_type, b0 + q);
+            const double av = std::fabs(v);
+            if (q == 0) mag = av;
+            if (!(av == mag) || av == 0.0 || std::isnan(v)) single = false;
+        }
+    }
+    for (int64_t j = 0; j < m; ++j)
+        if (ptr_at(indptr, indptr_type, j + 1) < ptr_at(indptr, indptr_type, j))
+            return fail(RP_ERR_INVALID, "R indptr not monotone");
+    if (layout == RP_LAYOUT_PACKED && !single)
+        return fail(RP_ERR_UNSUPPORTED, "R does not qualify for the packed layout");
+    const bool packed = single && layout != RP_LAYOUT_GENERIC;
+
+    rp_projector* h = new (std::nothrow) rp_projector();
+    if (!h) return fail(RP_ERR_NOMEM, "out of host memory");
+    h->device = device;
+    h->m = m;
+    h->p = p;
+    h->nnz = nnz;
+    h->value_type = data_type;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete h;
+        return fail(RP_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+    }
+    int rc = RP_OK;
+    if (packed) {
+        h->layout = RP_LAYOUT_PACKED;
+        h->mag = mag;
+        // block shift: every block's overflow region must be addressable with 15 bits
+        int bs = 12;
+        std::vector<uint64_t> need;
+        for (;; --bs) {
+            const int64_t nb = (m + ((int64_t)1 << bs) - 1) >> bs;
+            need.assign((size_t)std::max<int64_t>(nb, 1), 0);
+            bool ok = true;
+            for (int64_t j = 0; j < m; ++j) {
+                const int64_t cnt = ptr_at(indptr, indptr_type, j + 1) - ptr_at(indptr, indptr_type, j);
+                if (cnt >= 2) need[(size_t)(j >> bs)] += 1 + (uint64_t)cnt;
+            }
+            for (uint64_t v : need) ok &= v <= 32767;
+            if (ok || bs == 0) break;
+        }
+        h->bs = bs;
+        const int64_t nb = (int64_t)need.size();
+        std::vector<uint32_t> base((size_t)nb);
+        uint64_t acc = 0;
+        for (int64_t b = 0; b < nb; ++b) {
+            base[(size_t)b] = (uint32_t)acc;
+            acc += need[(size_t)b];
+        }
+        if (acc >= ((uint64_t)1 << 32)) { delete h; return fail(RP_ERR_UNSUPPORTED, "overflow table too large"); }
+        std::vector<uint16_t> W((size_t)std::max<int64_t>(m, 1), 0);
+        std::vector<uint16_t> O((size_t)std::max<uint64_t>(acc, 1), 0);
+        std::vector<uint64_t> fill(base.begin(), base.end());
+        for (int64_t j = 0; j < m; ++j) {
+            const int64_t s = ptr_at(indptr, indptr_type, j), t = ptr_at(indptr, indptr_type, j + 1);
+            const int64_t cnt = t - s;
+            if (cnt == 1) {
+                const uint32_t col = (uint32_t)ptr_at(indices, indices_type, s);
+                const bool neg = val_at(data, data_type, s) < 0;
+                W[(size_t)j] = (uint16_t)(0x4000u | (neg ? 0x2000u : 0u) | col);
+            } else if (cnt >= 2) {
+                const size_t b = (size_t)(j >> bs);
+                const uint64_t rec = fill[b];
+                W[(size_t)j] = (uint16_t)(0x8000u | (uint32_t)(rec - base[b]));
+                O[rec] = (uint16_t)cnt;
+                for (int64_t q = 0; q < cnt; ++q) {
+                    const uint32_t col = (uint32_t)ptr_at(indices, indices_type, s + q);
+                    const bool neg = val_at(data, data_type, s + q) < 0;
+                    O[rec + 1 + (uint64_t)q] = (uint16_t)((neg ? 0x8000u : 0u) | col);
+                }
+                fill[b] += 1 + (uint64_t)cnt;
+            }
+        }
+        if ((rc = h->W.ensure(2 * W.size(), device)) || (rc = h->base.ensure(4 * base.size(), device)) ||
+            (rc = h->O.ensure(2 * O.size(), device))) {
+            delete h;
+            return rc;
+        }
+        h->W.bytes = 2 * (size_t)m;
+        h->base.bytes = 4 * base.size();
+        h->O.bytes = 2 * (size_t)acc;
+        e = hipMemcpy(h->W.p, W.data(), 2 * W.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(h->base.p, base.data(), 4 * base.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(h->O.p, O.data(), 2 * O.size(), hipMemcpyHostToDevice);
+    } else {
+        h->layout = RP_LAYOUT_GENERIC;
+        std::vector<int32_t> Bp((size_t)m + 1);
+        std::vector<uint16_t> Bj((size_t)std::max<int64_t>(nnz, 1));
+        for (int64_t j = 0; j <= m; ++j) Bp[(size_t)j] = (int32_t)(ptr_at(indptr, indptr_type, j) - b0);
+        for (int64_t q = 0; q < nnz; ++q) Bj[(size_t)q] = (uint16_t)ptr_at(indices, indices_type, b0 + q);
+        if ((rc = h->Bp.ensure(4 * Bp.size(), device)) || (rc = h->Bj.ensure(2 * Bj.size(), device))) {
+            delete h;
+            return rc;
+        }
+        h->Bp.bytes = 4 * Bp.size();
+        h->Bj.bytes = 2 * (size_t)nnz;
+        e = hipMemcpy(h->Bp.p, Bp.data(), 4 * Bp.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(h->Bj.p, Bj.data(), 2 * Bj.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess) {
+            DevBuf& dst = data_type == RP_F64 ? h->Bx64 : h->Bx32;
+            const size_t vs = (size_t)dtype_size(data_type);
+            if ((rc = dst.ensure(vs * (size_t)std::max<int64_t>(nnz, 1), device))) {
+                delete h;
+                return rc;
+            }
+            dst.bytes = vs * (size_t)nnz;
+            if (nnz > 0)
+                e = hipMemcpy(dst.p, (const char*)data + vs * (size_t)b0, vs * (size_t)nnz, hipMemcpyHostToDevice);
+        }
+    }
+    if (e != hipSuccess) {
+        delete h;
+        return fail(RP_ERR_HIP, "R upload failed: %s", hipGetErrorString(e));
+    }
+    *out = h;
+    return RP_OK;
+}
+
+int rp_projector_info_get(const rp_projector* h, rp_projector_info* out) {
+    if (!h || !out) return fail(RP_ERR_INVALID, "NULL argument");
+    std::memset(out, 0, sizeof *out);
+    out->m = h->m;
+    out->p = h->p;
+    out->nnz = h->nnz;
+    out->layout = h->layout;
+    out->value_type = h->value_type;
+    out->magnitude = h->mag;
+    out->block_shift = h->bs;
+    if (h->layout == RP_LAYOUT_PACKED) {
+        out->n_buffers = 3;
+        out->buffer_bytes[0] = (int64_t)h->W.bytes;
+        out->buffer_bytes[1] = (int64_t)h->base.bytes;
+        out->buffer_bytes[2] = (int64_t)h->O.bytes;
+    } else {
+        out->n_buffers = 3;
+        out->buffer_bytes[0] = (int64_t)h->Bp.bytes;
+        out->buffer_bytes[1] = (int64_t)h->Bj.bytes;
+        const DevBuf& bx = h->value_type == RP_F64 ? h->Bx64 : h->Bx32;
+        out->buffer_bytes[2] = (int64_t)bx.bytes;
+    }
+    return RP_OK;
+}
+
+static const DevBuf* image_buffer(const rp_projector* h, int which) {
+    if (h->layout == RP_LAYOUT_PACKED) {
+        const DevBuf* b[3] = {&h->W, &h->base, &h->O};
+        return (which >= 0 && which < 3) ? b[which] : nullptr;
+    }
+    const DevBuf* b[3] = {&h->Bp, &h->Bj, h->value_type == RP_F64 ? &h->Bx64 : &h->Bx32};
+    return (which >= 0 && which < 3) ? b[which] : nullptr;
+}
+
+int rp_projector_export(const rp_projector* h, int32_t which, void* dst_device, void* stream) {
+    if (!h || !dst_device) return fail(RP_ERR_INVALID, "NULL argument");
+    const DevBuf* b = image_buffer(h, which);
+    if (!b) return fail(RP_ERR_INVALID, "buffer index %d out of range", which);
+    HIP_TRY(hipSetDevice(h->device));
+    if (b->bytes)
+        HIP_TRY(hipMemcpyAsync(dst_device, b->p, b->bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    return RP_OK;
+}
+
+int rp_projector_create_from_device(int device, const rp_projector_info* info,
+                                    const void* const* buffers, rp_projector** out) {
+    if (!info || !buffers || !out) return fail(RP_ERR_INVALID, "NULL argument");
+    *out = nullptr;
+    if (info->layout != RP_LAYOUT_PACKED && info->layout != RP_LAYOUT_GENERIC)
+        return fail(RP_ERR_INVALID, "bad layout");
+    rp_projector* h = new (std::nothrow) rp_projector();
+    if (!h) return fail(RP_ERR_NOMEM, "out of host memory");
+    h->device = device;
+    h->m = info->m;
+    h->p = info->p;
+    h->nnz = info->nnz;
+    h->layout = info->layout;
+    h->value_type = info->value_type;
+    h->mag = info->magnitude;
+    h->bs = info->block_shift;
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete h;
+        return fail(RP_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
+    }
+    DevBuf* dst[3];
+    if (h->layout == RP_LAYOUT_PACKED) {
+        dst[0] = &h->W; dst[1] = &h->base; dst[2] = &h->O;
+    } else {
+        dst[0] = &h->Bp; dst[1] = &h->Bj; dst[2] = h->value_type == RP_F64 ? &h->Bx64 : &h->Bx32;
+    }
+    for (int i = 0; i < 3; ++i) {
+        int rc = dst[i]->ensure((size_t)std::max<int64_t>(info->buffer_bytes[i], 2), device);
+        if (rc) { delete h; return rc; }
+        dst[i]->bytes = (size_t)info->buffer_bytes[i];
+        if (info->buffer_bytes[i] > 0) {
+            e = hipMemcpy(dst[i]->p, buffers[i], (size_t)info->buffer_bytes[i], hipMemcpyDeviceToDevice);
+            if (e != hipSuccess) { delete h; return fail(RP_ERR_HIP, "image copy: %s", hipGetErrorString(e)); }
+        }
+    }
+    *out = h;
+    return RP_OK;
+}
+
+int rp_projector_destroy(rp_projector* h) {
+    delete h;
+    return RP_OK;
+}
+
+int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows) {
+    (void)h;
+    const int64_t tiles = n_rows > 0 ? (n_rows + 1 - 1) : 1;  // worst case rpt = 1
+    return (int64_t)sizeof(Workspace) + 8 * tiles;
+}
+
+int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int32_t order,
+                      void* workspace, void* stream, int64_t* total_nnz) {
+    if (!h) return fail(RP_ERR_INVALID, "NULL projector");
+    if (order != RP_ORDER_SCIPY && order != RP_ORDER_SORTED) return fail(RP_ERR_INVALID, "bad order");
+    // nnz(A) for tile sizing: given, or read from the two ends of indptr (tiny D2H)
+    int64_t nnz_a = a ? a->nnz : -1;
+    if (a && nnz_a < 0 && a->n_rows > 0 && a->indptr) {
+        HIP_TRY(hipSetDevice(h->device));
+        const int es = dtype_size(a->indptr_type);
+        if (es == 0) return fail(RP_ERR_INVALID, "bad indptr type");
+        int64_t first = 0, last = 0;
+        HIP_TRY(hipMemcpyAsync(&first, a->indptr, es, hipMemcpyDeviceToHost, (hipStream_t)stream));
+        HIP_TRY(hipMemcpyAsync(&last, (const char*)a->indptr + es * a->n_rows, es, hipMemcpyDeviceToHost,
+                               (hipStream_t)stream));
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+        if (es == 4) {
+            first = (int32_t)first;
+            last = (int32_t)last;
+        }
+        nnz_a = last - first;
+    }
+    return project_device_impl(h, a, c, order, workspace, (hipStream_t)stream, total_nnz, nnz_a);
+}
+
+int rp_project_host_begin(rp_projector* h, const rp_csr_in* a, int32_t order, rp_result** out,
+                          int64_t* nnz) {
+    if (!h || !a || !out || !nnz) return fail(RP_ERR_INVALID, "NULL argument");
+    if (order != RP_ORDER_SCIPY && order != RP_ORDER_SORTED) return fail(RP_ERR_INVALID, "bad order");
+    *out = nullptr;
+    const int ips = dtype_size(a->indptr_type), vs = dtype_size(a->data_type);
+    if (!ips || (a->data_type != RP_F32 && a->data_type != RP_F64)) return fail(RP_ERR_INVALID, "bad A types");
+    if (a->n_rows < 0 || !a->indptr) return fail(RP_ERR_INVALID, "bad A");
+    const int64_t n = a->n_rows;
+    const int64_t b0 = ptr_at(a->indptr, a->indptr_type, 0);
+    const int64_t nnz_a = ptr_at(a->indptr, a->indptr_type, n) - b0;
+    if (nnz_a < 0) return fail(RP_ERR_INVALID, "A indptr decreasing");
+    for (int64_t q = 0; q < nnz_a; ++q) {
+        const int32_t j = a->indices[b0 + q];
+        if (j < 0 || j >= h->m)
+            return fail(RP_ERR_INVALID, "A column index %d out of range [0, %lld)", j, (long long)h->m);
+    }
+    std::lock_guard<std::mutex> lock(h->mu);
+    HIP_TRY(hipSetDevice(h->device));
+    rp_result* r = new (std::nothrow) rp_result();
+    if (!r) return fail(RP_ERR_NOMEM, "out of host memory");
+    r->h = h;
+    r->n_rows = n;
+    r->value_type = a->data_type;
+    int rc;
+    // upload A (indptr rebased to 0, as int64)
+    if ((rc = h->a_ptr.ensure(8 * (size_t)(n + 1), h->device)) ||
+        (rc = h->a_idx.ensure(4 * (size_t)std::max<int64_t>(nnz_a, 1), h->device)) ||
+        (rc = h->a_val.ensure((size_t)vs * (size_t)std::max<int64_t>(nnz_a, 1), h->device))) {
+        delete r;
+        return rc;
+    }
+    std::vector<int64_t> ptr64((size_t)n + 1);
+    for (int64_t i = 0; i <= n; ++i) ptr64[(size_t)i] = ptr_at(a->indptr, a->indptr_type, i) - b0;
+    hipError_t e = hipMemcpy(h->a_ptr.p, ptr64.data(), 8 * (size_t)(n + 1), hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz_a > 0)
+        e = hipMemcpy(h->a_idx.p, a->indices + b0, 4 * (size_t)nnz_a, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nnz_a > 0)
+        e = hipMemcpy(h->a_val.p, (const char*)a->data + (size_t)vs * (size_t)b0, (size_t)vs * (size_t)nnz_a,
+                      hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        delete r;
+        return fail(RP_ERR_HIP, "A upload: %s", hipGetErrorString(e));
+    }
+    rp_csr_in ad{n, h->a_ptr.p, RP_I64, (const int32_t*)h->a_idx.p, h->a_val.p, a->data_type, nnz_a};
+    // capacity guess from the expected products, exact retry on overflow
+    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    int64_t cap = (int64_t)(1.25 * ppe * (double)nnz_a) + 1024;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        if ((rc = r->cp.ensure(8 * (size_t)(n + 1), h->device)) ||
+            (rc = r->cj.ensure(4 * (size_t)cap, h->device)) ||
+            (rc = r->cx.ensure((size_t)vs * (size_t)cap, h->device))) {
+            delete r;
+            return rc;
+        }
+        rp_csr_out cd{r->cp.p, RP_I64, r->cj.p, RP_I32, r->cx.p, cap};
+        int64_t total = 0;
+        rc = project_device_impl(h, &ad, &cd, order, nullptr, nullptr, &total, nnz_a);
+        if (rc == RP_ERR_CAPACITY && attempt == 0) {
+            cap = total;
+            continue;
+        }
+        if (rc) {
+            delete r;
+            return rc;
+        }
+        r->nnz = total;
+        break;
+    }
+    *nnz = r->nnz;
+    *out = r;
+    return RP_OK;
+}
+
+int rp_result_fetch(rp_result* r, void* indptr, int32_t indptr_type, void* indices,
+                    int32_t indices_type, void* data) {
+    if (!r || !indptr) return fail(RP_ERR_INVALID, "NULL argument");
+    if ((indptr_type != RP_I32 && indptr_type != RP_I64) || (indices_type != RP_I32 && indices_type != RP_I64))
+        return fail(RP_ERR_INVALID, "bad index type");
+    if (r->nnz > 0 && (!indices || !data)) return fail(RP_ERR_INVALID, "NULL output arrays");
+    HIP_TRY(hipSetDevice(r->h->device));
+    const int64_t n = r->n_rows;
+    if (indptr_type == RP_I64) {
+        HIP_TRY(hipMemcpy(indptr, r->cp.p, 8 * (size_t)(n + 1), hipMemcpyDeviceToHost));
+    } else {
+        std::vector<int64_t> tmp((size_t)n + 1);
+        HIP_TRY(hipMemcpy(tmp.data(), r->cp.p, 8 * (size_t)(n + 1), hipMemcpyDeviceToHost));
+        int32_t* o = (int32_t*)indptr;
+        for (int64_t i = 0; i <= n; ++i) o[i] = (int32_t)tmp[(size_t)i];
+    }
+    if (r->nnz > 0) {
+        if (indices_type == RP_I32) {
+            HIP_TRY(hipMemcpy(indices, r->cj.p, 4 * (size_t)r->nnz, hipMemcpyDeviceToHost));
+        } else {
+            std::vector<int32_t> tmp((size_t)r->nnz);
+            HIP_TRY(hipMemcpy(tmp.data(), r->cj.p, 4 * (size_t)r->nnz, hipMemcpyDeviceToHost));
+            int64_t* o = (int64_t*)indices;
+            for (int64_t i = 0; i < r->nnz; ++i) o[i] = tmp[(size_t)i];
+        }
+        HIP_TRY(hipMemcpy(data, r->cx.p, (size_t)dtype_size(r->value_type) * (size_t)r->nnz,
+                          hipMemcpyDeviceToHost));
+    }
+    return RP_OK;
+}
+
+int rp_result_free(rp_result* r) {
+    delete r;
+    return RP_OK;
+}
+
+int rp_synth_rows_device(int device, int64_t n_rows, int64_t m, double mean_extra,
+                         int32_t max_row_nnz, int32_t dist, double zipf_s, uint64_t seed,
+                         void* indptr, int32_t indptr_type, int32_t* indices, float* data,
+                         void* stream, int64_t* nnz) {
+    if (!indptr || n_rows < 0 || m <= 0 || !nnz) return fail(RP_ERR_INVALID, "bad argument");
+    if (indptr_type != RP_I32 && indptr_type != RP_I64) return fail(RP_ERR_INVALID, "bad indptr type");
+    if (max_row_nnz < 1 || max_row_nnz > kSynthMaxK) return fail(RP_ERR_INVALID, "max_row_nnz in [1, %d]", kSynthMaxK);
+    if (dist != 0 && dist != 1) return fail(RP_ERR_INVALID, "dist must be 0 (uniform) or 1 (power-law)");
+    if (dist == 1 && !(zipf_s > 1.0)) return fail(RP_ERR_INVALID, "zipf_s must be > 1");
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t st = (hipStream_t)stream;
+    DevBuf ptr64, tmp;
+    int rc = ptr64.ensure(8 * (size_t)(n_rows + 1), device);
+    if (rc) return rc;
+    HIP_TRY(hipMemsetAsync(ptr64.p, 0, 8, st));
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_rows + 255) / 256, 1), 65536);
+    hipLaunchKernelGGL((synth_count_kernel<int64_t>), dim3(grid), dim3(256), 0, st, n_rows, seed,
+                       mean_extra, max_row_nnz, m, (int64_t*)ptr64.p);
+    HIP_TRY(hipGetLastError());
+    rc = inclusive_scan_i64((int64_t*)ptr64.p + 1, n_rows, st, tmp, device);
+    if (rc) return rc;
+    int64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, (int64_t*)ptr64.p + n_rows, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (indptr_type == RP_I32 && total >= ((int64_t)1 << 31))
+        return fail(RP_ERR_UNSUPPORTED, "nnz %lld needs int64 indptr", (long long)total);
+    if (indptr_type == RP_I64) {
+        HIP_TRY(hipMemcpyAsync(indptr, ptr64.p, 8 * (size_t)(n_rows + 1), hipMemcpyDeviceToDevice, st));
+    } else {
+        hipLaunchKernelGGL((convert_kernel<int64_t, int32_t>), dim3(grid), dim3(256), 0, st,
+                           (const int64_t*)ptr64.p, (int32_t*)indptr, n_rows + 1);
+        HIP_TRY(hipGetLastError());
+    }
+    if (indices) {
+        if (!data) return fail(RP_ERR_INVALID, "NULL data");
+        const uint64_t perm_b = (seed * 0x9E3779B97F4A7C15ull) % (uint64_t)m;
+        uint64_t perm_a = 2654435761ull % (uint64_t)m;
+        auto gcd = [](uint64_t x, uint64_t y) { while (y) { uint64_t t = x % y; x = y; y = t; } return x; };
+        while (perm_a == 0 || gcd(perm_a, (uint64_t)m) != 1) perm_a = (perm_a + 1) % (uint64_t)m;
+        hipLaunchKernelGGL(synth_fill_kernel, dim3(grid), dim3(256), 0, st, n_rows, m, seed, dist, zipf_s,
+                           perm_a, perm_b, (const int64_t*)ptr64.p, indices, data);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    *nnz = total;
+    return RP_OK;
+}
+
+}  // extern "C"

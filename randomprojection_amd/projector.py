@@ -1,0 +1,251 @@
+"""R resident on one MI355X and the product ``A @ R`` computed by librp's HIP kernel.
+
+Replaces, in the reference (paths relative to /root/reference):
+  * ``local_rnd_mat = srp.components_.T.astype(np.float32)``   code/clustermode/randomProjection.py:101
+  * ``sc.broadcast(local_rnd_mat)``                              code/clustermode/randomProjection.py:104
+  * ``features_matrix.dot(local_csr_matrix)``                    code/clustermode/randomProjection.py:46
+    -> scipy ``_matmul_sparse`` (scipy/sparse/_compressed.py:546-604): ``other = self.__class__(other)``
+       then ``csr_matmat_maxnnz`` + ``csr_matmat``.
+
+``Projector.matmul(A)`` returns exactly what ``A @ R`` returns in scipy for CSR ``A``: same
+container type, same value dtype (``upcast``), same index dtype rule (``get_index_dtype`` with
+``check_contents=False``), same per-row storage order, same values bit for bit.
+There is no CPU fallback: a missing library or GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+import weakref
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _native as nat
+
+__all__ = ["Projector", "get_projector", "scipy_result_index_dtype"]
+
+_INT32_MAX = np.iinfo(np.int32).max
+
+
+def _operand_csr(R) -> sp.csr_matrix:
+    """scipy's ``other = self.__class__(other)`` (scipy/sparse/_compressed.py:564): a CSR view of a
+    CSR input (storage order kept), ``csc_tocsr`` for CSC (rows sorted by column), ``tocsr`` else."""
+    if sp.issparse(R):
+        return R if (R.format == "csr" and isinstance(R, sp.csr_matrix)) else sp.csr_matrix(R)
+    R = np.asarray(R)
+    if R.ndim != 2:
+        raise ValueError("R must be 2-D")
+    return sp.csr_matrix(R)
+
+
+def scipy_result_index_dtype(arrays, nnz) -> np.dtype:
+    """``_get_index_dtype(arrays, maxval=nnz)`` of ``_matmul_sparse`` (check_contents=False)."""
+    if nnz > _INT32_MAX:
+        return np.dtype(np.int64)
+    for a in arrays:
+        if not np.can_cast(np.asarray(a).dtype, np.int32):
+            return np.dtype(np.int64)
+    return np.dtype(np.int32)
+
+
+class Projector:
+    """An m x p projection matrix R uploaded once to ``device`` (HBM resident).
+
+    ``layout``: "auto" (packed single-magnitude layout when R qualifies — every
+    SparseRandomProjection matrix does — else generic CSR), "packed" or "generic".
+    """
+
+    def __init__(self, R=None, device: int = 0, layout: str = "auto", *, _handle=None, _meta=None):
+        self._lib = nat.load()
+        self._lock = threading.Lock()
+        self.device = int(device)
+        if _handle is not None:
+            self._h = _handle
+            self.r_index_dtype, self.dtype = _meta
+        else:
+            Rc = _operand_csr(R)
+            if Rc.dtype not in (np.float32, np.float64):
+                Rc = Rc.astype(np.float64)
+            self.r_index_dtype = np.result_type(Rc.indptr.dtype, Rc.indices.dtype)
+            self.dtype = Rc.dtype
+            code = {"auto": nat.RP_LAYOUT_AUTO, "generic": nat.RP_LAYOUT_GENERIC, "packed": nat.RP_LAYOUT_PACKED}[layout]
+            indptr = np.ascontiguousarray(Rc.indptr)
+            indices = np.ascontiguousarray(Rc.indices)
+            data = np.ascontiguousarray(Rc.data)
+            h = ctypes.c_void_p()
+            nat.check(self._lib.rp_projector_create(
+                self.device, Rc.shape[0], Rc.shape[1], nat.ptr(indptr), nat.idx_code(indptr.dtype),
+                nat.ptr(indices), nat.idx_code(indices.dtype), nat.ptr(data), nat.val_code(data.dtype),
+                code, ctypes.byref(h)))
+            self._h = h
+        info = nat.ProjectorInfo()
+        nat.check(self._lib.rp_projector_info_get(self._h, ctypes.byref(info)))
+        self.info = info
+        self.m, self.p, self.nnz = int(info.m), int(info.p), int(info.nnz)
+        self.layout = "packed" if info.layout == nat.RP_LAYOUT_PACKED else "generic"
+        self.shape = (self.m, self.p)
+
+    # -------------------------------------------------------------------------------- lifetime
+    def close(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.rp_projector_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------------------------- image
+    def image_nbytes(self):
+        return [int(self.info.buffer_bytes[i]) for i in range(self.info.n_buffers)]
+
+    def export_image(self, dst_ptrs, stream=0):
+        """Copy the device image into caller device buffers (e.g. torch tensors to broadcast)."""
+        for i, dst in enumerate(dst_ptrs):
+            nat.check(self._lib.rp_projector_export(self._h, i, ctypes.c_void_p(int(dst)), ctypes.c_void_p(stream)))
+
+    @classmethod
+    def from_image(cls, info: "nat.ProjectorInfo", src_ptrs, device: int, r_index_dtype=np.int32, dtype=np.float32):
+        """Build a projector from an image already in device memory (after an RCCL broadcast)."""
+        lib = nat.load()
+        arr = (ctypes.c_void_p * len(src_ptrs))(*[ctypes.c_void_p(int(s)) for s in src_ptrs])
+        h = ctypes.c_void_p()
+        nat.check(lib.rp_projector_create_from_device(int(device), ctypes.byref(info), arr, ctypes.byref(h)))
+        return cls(device=device, _handle=h, _meta=(np.dtype(r_index_dtype), np.dtype(dtype)))
+
+    # -------------------------------------------------------------------------------- host path
+    def compute_dtype(self, a_dtype) -> np.dtype:
+        T = np.result_type(np.dtype(a_dtype), self.dtype)
+        if T == np.float16:
+            T = np.dtype(np.float32)
+        if T not in (np.float32, np.float64):
+            raise TypeError(f"unsupported value dtype {T} (float32/float64 only)")
+        return np.dtype(T)
+
+    def project_arrays(self, indptr, indices, data, n_cols=None, order: str = "scipy", out_index_dtype=None):
+        """CSR arrays in (host), CSR arrays out (host): (indptr, indices, data)."""
+        if n_cols is not None and n_cols != self.m:
+            raise ValueError(f"matmul: dimension mismatch with signature (n,k={n_cols}),(k={self.m},m)->(n,m)")
+        indptr = np.asarray(indptr)
+        indices = np.asarray(indices)
+        T = self.compute_dtype(np.asarray(data).dtype)
+        data = np.ascontiguousarray(data, dtype=T)
+        if indptr.dtype not in (np.int32, np.int64):
+            indptr = indptr.astype(np.int64)
+        indptr = np.ascontiguousarray(indptr)
+        aj = np.ascontiguousarray(indices, dtype=np.int32) if indices.dtype != np.int32 else np.ascontiguousarray(indices)
+        if indices.dtype != np.int32 and indices.size and (indices.min() < 0 or indices.max() >= self.m):
+            raise ValueError("column index out of range")
+        n = len(indptr) - 1
+        a = nat.CsrIn(n, nat.ptr(indptr).value, nat.idx_code(indptr.dtype), nat.ptr(aj).value,
+                      nat.ptr(data).value, nat.val_code(T), int(indptr[-1] - indptr[0]) if n >= 0 else 0)
+        res = ctypes.c_void_p()
+        nnz = ctypes.c_int64(0)
+        code = nat.RP_ORDER_SORTED if order == "sorted" else nat.RP_ORDER_SCIPY
+        with self._lock:
+            rc = self._lib.rp_project_host_begin(self._h, ctypes.byref(a), code, ctypes.byref(res), ctypes.byref(nnz))
+            if rc == nat.RP_ERR_INVALID:
+                raise ValueError(self._lib.rp_last_error().decode())
+            nat.check(rc)
+            try:
+                k = int(nnz.value)
+                if out_index_dtype is None:
+                    out_index_dtype = scipy_result_index_dtype((indptr, indices), k)
+                    if self.r_index_dtype == np.int64:
+                        out_index_dtype = np.dtype(np.int64)
+                out_index_dtype = np.dtype(out_index_dtype)
+                Cp = np.empty(n + 1, dtype=out_index_dtype)
+                Cj = np.empty(k, dtype=out_index_dtype)
+                Cx = np.empty(k, dtype=T)
+                nat.check(self._lib.rp_result_fetch(res, nat.ptr(Cp), nat.idx_code(out_index_dtype), nat.ptr(Cj),
+                                                    nat.idx_code(out_index_dtype), nat.ptr(Cx)))
+            finally:
+                self._lib.rp_result_free(res)
+        return Cp, Cj, Cx
+
+    def matmul(self, A, order: str = "scipy"):
+        """``A @ R`` for sparse A, returning what scipy returns (container of A's class)."""
+        if not sp.issparse(A):
+            raise TypeError("Projector.matmul expects a scipy sparse matrix/array")
+        if A.shape[1] != self.m:
+            raise ValueError(f"matmul: dimension mismatch with signature (n,k={A.shape[1]}),(k={self.m},m)->(n,m)")
+        cls = A.__class__ if A.format == "csr" else (sp.csr_array if isinstance(A, sp.sparray) else sp.csr_matrix)
+        Ac = A if A.format == "csr" else A.tocsr()
+        T = self.compute_dtype(Ac.dtype)
+        Cp, Cj, Cx = self.project_arrays(Ac.indptr, Ac.indices, Ac.data.astype(T, copy=False), order=order)
+        return cls((Cx, Cj, Cp), shape=(Ac.shape[0], self.p))
+
+    # -------------------------------------------------------------------------------- device path
+    def project_device(self, Ap, Aj, Ax, Cp, Cj, Cx, order: str = "scipy", stream=0, workspace=None,
+                       nnz_a: int = -1, sync: bool = True):
+        """Device-resident product on raw device pointers or torch tensors.
+
+        Returns the exact output nnz when ``sync`` (raises ``RPError`` with code RP_ERR_CAPACITY
+        if ``Cj``/``Cx`` are too small), else None (fully asynchronous launch on ``stream``)."""
+        def p_(t):
+            return int(t.data_ptr()) if hasattr(t, "data_ptr") else int(t)
+
+        def code_(t, ints=True):
+            dt = str(getattr(t, "dtype", ""))
+            if ints:
+                return nat.RP_I64 if dt.endswith("int64") else nat.RP_I32
+            return nat.RP_F64 if dt.endswith("float64") else nat.RP_F32
+
+        n = (Ap.numel() if hasattr(Ap, "numel") else len(Ap)) - 1
+        cap = Cj.numel() if hasattr(Cj, "numel") else len(Cj)
+        a = nat.CsrIn(n, p_(Ap), code_(Ap), p_(Aj), p_(Ax), code_(Ax, False), int(nnz_a))
+        c = nat.CsrOut(p_(Cp), code_(Cp), p_(Cj), code_(Cj), p_(Cx), int(cap))
+        total = ctypes.c_int64(0)
+        code = nat.RP_ORDER_SORTED if order == "sorted" else nat.RP_ORDER_SCIPY
+        rc = self._lib.rp_project_device(self._h, ctypes.byref(a), ctypes.byref(c), code,
+                                         ctypes.c_void_p(p_(workspace) if workspace is not None else 0),
+                                         ctypes.c_void_p(stream), ctypes.byref(total) if sync else None)
+        if rc == nat.RP_ERR_CAPACITY:
+            err = nat.RPError(rc, self._lib.rp_last_error().decode())
+            err.nnz = int(total.value)
+            raise err
+        nat.check(rc)
+        return int(total.value) if sync else None
+
+    def __repr__(self):
+        return f"Projector(m={self.m}, p={self.p}, nnz={self.nnz}, layout={self.layout}, device={self.device})"
+
+
+# ------------------------------------------------------------------------------------------------
+# projector cache for the drop-ins: one upload per R object (the broadcast-once of the recipe)
+_cache: "dict[int, tuple]" = {}
+_cache_lock = threading.Lock()
+
+
+def _fingerprint(R):
+    if sp.issparse(R):
+        arrs = [getattr(R, n, None) for n in ("data", "indices", "indptr")]
+        ptrs = tuple((a.__array_interface__["data"][0], a.size) if isinstance(a, np.ndarray) else None for a in arrs)
+        return (R.format, R.shape, R.nnz, str(R.dtype), ptrs)
+    a = np.asarray(R)
+    return ("dense", a.shape, str(a.dtype), a.__array_interface__["data"][0])
+
+
+def get_projector(R, device: int = 0) -> Projector:
+    """The resident projector for ``R`` (a scipy matrix, or a ``Projector`` passed through)."""
+    if isinstance(R, Projector):
+        return R
+    key = id(R)
+    fp = _fingerprint(R)
+    with _cache_lock:
+        hit = _cache.get(key)
+        if hit is not None and hit[1] == fp and hit[2] == device:
+            ref = hit[0]()
+            if ref is not None:
+                return hit[3]
+    proj = Projector(R, device=device)
+    try:
+        ref = weakref.ref(R, lambda _r, k=key: _cache.pop(k, None))
+    except TypeError:
+        ref = lambda: R  # noqa: E731 - objects without weakref support stay cached
+    with _cache_lock:
+        _cache[key] = (ref, fp, device, proj)
+    return proj

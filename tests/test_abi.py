@@ -1,0 +1,41 @@
+"""The C-ABI library (librp.so) loads without a GPU and exports every symbol include/rp.h declares."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+from randomprojection_amd import _native as nat
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "rp.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rp_[a-z_]+)\s*\(", src)))
+
+
+def test_header_matches_binding_table():
+    assert _declared() == sorted(nat.EXPORTS)
+
+
+def test_library_exports_all_symbols():
+    lib = ctypes.CDLL(nat.LIB_PATH)
+    for name in _declared():
+        assert hasattr(lib, name), name
+
+
+def test_calls_without_gpu_fail_loudly():
+    lib = nat.load()
+    assert lib.rp_version().startswith(b"rp-mi355x")
+    n = ctypes.c_int(-1)
+    rc = lib.rp_device_count(ctypes.byref(n))
+    if rc != nat.RP_OK:                       # CPU container: error + message, never a crash
+        assert n.value == 0 and lib.rp_last_error()
+
+
+def test_invalid_arguments_rejected_before_device_use():
+    lib = nat.load()
+    h = ctypes.c_void_p()
+    rc = lib.rp_projector_create(0, 10, 0, None, nat.RP_I32, None, nat.RP_I32, None, nat.RP_F32, 0, ctypes.byref(h))
+    assert rc == nat.RP_ERR_INVALID and b"bad shape" in lib.rp_last_error()
+    rc = lib.rp_projector_create(0, 10, 40000, None, nat.RP_I32, None, nat.RP_I32, None, nat.RP_F32, 0, ctypes.byref(h))
+    assert rc in (nat.RP_ERR_INVALID, nat.RP_ERR_UNSUPPORTED)
