@@ -1,0 +1,107 @@
+"""Multi-process (world_size 2, gloo, CPU) coverage of the sharded driver's host protocol: shard
+planning, the R-image broadcast (metadata + byte buffers), the all_gather of shard nnz and the
+global offsets. Per-shard products here come from the oracle (test-side stand-in for the GPU)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from randomprojection_amd.driver import broadcast_image, exclusive_offsets, plan_shards
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _matrix(seed=0, n=3000, m=20_000):
+    rng = np.random.default_rng(seed)
+    k = 1 + rng.poisson(10, n)
+    k[::97] = 0
+    cols = [np.unique(rng.integers(0, m, int(x))) for x in k]
+    indptr = np.concatenate([[0], np.cumsum([c.size for c in cols])])
+    return sp.csr_matrix((rng.standard_normal(indptr[-1]).astype(np.float32),
+                          np.concatenate(cols).astype(np.int32), indptr), shape=(n, m))
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from oracle import smmp
+        from randomprojection_amd import srp_matrix as sm
+
+        # R image broadcast: rank 0 owns the bytes, everyone receives them
+        R = sm.projection_operand(sm.sparse_random_matrix(128, 20_000, random_state=123))
+        blobs = [R.indptr.view(np.uint8), R.indices.view(np.uint8), R.data.view(np.uint8)]
+        meta = {"n_buffers": 3, "buffer_bytes": [b.size for b in blobs]} if rank == 0 else None
+        sizes = [b.size for b in blobs]
+        bufs = [torch.from_numpy(b.copy()) if rank == 0 else torch.zeros(s, dtype=torch.uint8)
+                for b, s in zip(blobs, sizes)]
+        got = broadcast_image(meta, bufs, src=0)
+        assert got["buffer_bytes"] == sizes
+        Rr = sp.csr_matrix((bufs[2].numpy().view(np.float32), bufs[1].numpy().view(np.int32),
+                            bufs[0].numpy().view(np.int32)), shape=R.shape)
+        assert (Rr != R).nnz == 0
+
+        # shard plan + per-shard product + global offsets
+        A = _matrix()
+        bounds = plan_shards(A.indptr, world)
+        r0, r1 = int(bounds[rank]), int(bounds[rank + 1])
+        Cp, Cj, Cx, _, _ = smmp.matmat(A[r0:r1], Rr)
+        t = torch.tensor([len(Cj)], dtype=torch.int64)
+        allc = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allc, t)
+        offs = exclusive_offsets([int(x) for x in allc])
+        parts = [None] * world
+        dist.all_gather_object(parts, (r0, int(offs[rank]), Cp.tolist(), Cj.tolist(), Cx.tolist()))
+        if rank == 0:
+            Fp, Fj, Fx, _, _ = smmp.matmat(A, R)
+            gp, gj, gx = [0], [], []
+            for (rs, no, cp, cj, cx) in parts:
+                assert no == len(gj)
+                gp.extend([no + v for v in cp[1:]])
+                gj.extend(cj)
+                gx.extend(cx)
+            assert np.array_equal(np.array(gp), Fp) and np.array_equal(np.array(gj), Fj)
+            assert np.array_equal(np.array(gx, np.float32), Fx)
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e)))
+
+
+def test_two_rank_gloo_protocol():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_plan_shards_balanced_and_covering(world):
+    A = _matrix(seed=world)
+    b = plan_shards(A.indptr, world)
+    assert b[0] == 0 and b[-1] == A.shape[0] and np.all(np.diff(b) >= 0) and len(b) == world + 1
+    nnz = np.diff(A.indptr[b])
+    assert nnz.max() - nnz.min() <= 2 * np.diff(A.indptr).max() + 1
+
+
+def test_plan_shards_degenerate():
+    assert list(plan_shards(np.zeros(5, np.int64), 2)) == [0, 2, 4]
+    assert list(plan_shards(np.array([0]), 4)) == [0, 0, 0, 0, 0]
