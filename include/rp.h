@@ -122,6 +122,14 @@ int rp_projector_create_from_device(int device, const rp_projector_info* info,
                                     const void* const* buffers, rp_projector** out);
 int rp_projector_destroy(rp_projector* h);
 
+/* Host-only (no GPU): build the device image of R that rp_projector_create would upload.
+ * Call with buf0..2 == NULL to get the layout and buffer sizes in *info, then again with caller
+ * buffers of info->buffer_bytes[i] bytes to receive W/base/records (packed) or Bp/Bj/values
+ * (generic). Lets a driver pack once and lets tests check the layout without a device. */
+int rp_pack_r_host(int64_t m, int64_t p, const void* indptr, int32_t indptr_type,
+                   const void* indices, int32_t indices_type, const void* data, int32_t data_type,
+                   int32_t layout, rp_projector_info* info, void* buf0, void* buf1, void* buf2);
+
 /* Workspace bytes rp_project_device needs for n_rows (look-back tile states + counters). */
 int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows);
 

@@ -868,6 +868,130 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
     return RP_OK;
 }
 
+// ---- host-side R image (packed single-magnitude layout, or generic CSR)
+struct HostImage {
+    int layout = RP_LAYOUT_GENERIC;
+    double mag = 0.0;
+    int bs = 0;
+    int64_t nnz = 0, b0 = 0;
+    std::vector<uint16_t> W;
+    std::vector<uint32_t> base;
+    std::vector<uint16_t> O;
+    std::vector<int32_t> Bp;
+    std::vector<uint16_t> Bj;
+};
+
+int build_image(int64_t m, int64_t p, const void* indptr, int32_t indptr_type, const void* indices,
+                int32_t indices_type, const void* data, int32_t data_type, int32_t layout,
+                HostImage& img) {
+    if (m < 0 || p <= 0) return fail(RP_ERR_INVALID, "bad shape (%lld, %lld)", (long long)m, (long long)p);
+    if (!indptr || (indptr_type != RP_I32 && indptr_type != RP_I64) ||
+        (indices_type != RP_I32 && indices_type != RP_I64) ||
+        (data_type != RP_F32 && data_type != RP_F64))
+        return fail(RP_ERR_INVALID, "bad R arrays");
+    if (layout != RP_LAYOUT_AUTO && layout != RP_LAYOUT_GENERIC && layout != RP_LAYOUT_PACKED)
+        return fail(RP_ERR_INVALID, "bad layout %d", layout);
+    if (p > 32767) return fail(RP_ERR_UNSUPPORTED, "p=%lld > 32767 not supported by the GPU path", (long long)p);
+    if (m >= ((int64_t)1 << 31)) return fail(RP_ERR_UNSUPPORTED, "m >= 2^31");
+    const int64_t b0 = ptr_at(indptr, indptr_type, 0);
+    const int64_t nnz = ptr_at(indptr, indptr_type, m) - b0;
+    if (nnz < 0 || nnz >= ((int64_t)1 << 31) - 1) return fail(RP_ERR_UNSUPPORTED, "R nnz out of range");
+    if (nnz > 0 && (!indices || !data)) return fail(RP_ERR_INVALID, "NULL R indices/data");
+    for (int64_t j = 0; j < m; ++j)
+        if (ptr_at(indptr, indptr_type, j + 1) < ptr_at(indptr, indptr_type, j))
+            return fail(RP_ERR_INVALID, "R indptr not monotone");
+    // validate columns and detect the single-magnitude layout
+    double mag = 0.0;
+    bool single = p <= 8192 && nnz > 0;
+    for (int64_t q = 0; q < nnz; ++q) {
+        const int64_t col = ptr_at(indices, indices_type, b0 + q);
+        if (col < 0 || col >= p) return fail(RP_ERR_INVALID, "R column index %lld out of range", (long long)col);
+        if (single) {
+            const double v = val_at(data, data_type, b0 + q);
+            const double av = std::fabs(v);
+            if (q == 0) mag = av;
+            if (!(av == mag) || av == 0.0 || std::isnan(v)) single = false;
+        }
+    }
+    if (layout == RP_LAYOUT_PACKED && !single)
+        return fail(RP_ERR_UNSUPPORTED, "R does not qualify for the packed layout");
+    img.nnz = nnz;
+    img.b0 = b0;
+    if (!(single && layout != RP_LAYOUT_GENERIC)) {
+        img.layout = RP_LAYOUT_GENERIC;
+        img.Bp.resize((size_t)m + 1);
+        img.Bj.resize((size_t)nnz);
+        for (int64_t j = 0; j <= m; ++j) img.Bp[(size_t)j] = (int32_t)(ptr_at(indptr, indptr_type, j) - b0);
+        for (int64_t q = 0; q < nnz; ++q) img.Bj[(size_t)q] = (uint16_t)ptr_at(indices, indices_type, b0 + q);
+        return RP_OK;
+    }
+    img.layout = RP_LAYOUT_PACKED;
+    img.mag = mag;
+    // block shift: every block's overflow region must be addressable with 15 bits
+    int bs = 12;
+    std::vector<uint64_t> need;
+    for (;; --bs) {
+        const int64_t nb = (m + ((int64_t)1 << bs) - 1) >> bs;
+        need.assign((size_t)std::max<int64_t>(nb, 1), 0);
+        for (int64_t j = 0; j < m; ++j) {
+            const int64_t cnt = ptr_at(indptr, indptr_type, j + 1) - ptr_at(indptr, indptr_type, j);
+            if (cnt >= 2) need[(size_t)(j >> bs)] += 1 + (uint64_t)cnt;
+        }
+        bool ok = true;
+        for (uint64_t v : need) ok &= v <= 32767;
+        if (ok || bs == 0) break;
+    }
+    img.bs = bs;
+    const int64_t nb = (int64_t)need.size();
+    img.base.resize((size_t)nb);
+    uint64_t acc = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+        img.base[(size_t)b] = (uint32_t)acc;
+        acc += need[(size_t)b];
+    }
+    if (acc >= ((uint64_t)1 << 31)) return fail(RP_ERR_UNSUPPORTED, "overflow table too large");
+    img.W.assign((size_t)m, 0);
+    img.O.assign((size_t)acc, 0);
+    std::vector<uint64_t> fill(img.base.begin(), img.base.end());
+    for (int64_t j = 0; j < m; ++j) {
+        const int64_t s0 = ptr_at(indptr, indptr_type, j), t0 = ptr_at(indptr, indptr_type, j + 1);
+        const int64_t cnt = t0 - s0;
+        if (cnt == 1) {
+            const uint32_t col = (uint32_t)ptr_at(indices, indices_type, s0);
+            const bool neg = val_at(data, data_type, s0) < 0;
+            img.W[(size_t)j] = (uint16_t)(0x4000u | (neg ? 0x2000u : 0u) | col);
+        } else if (cnt >= 2) {
+            const size_t b = (size_t)(j >> bs);
+            const uint64_t rec = fill[b];
+            img.W[(size_t)j] = (uint16_t)(0x8000u | (uint32_t)(rec - img.base[b]));
+            img.O[rec] = (uint16_t)cnt;
+            for (int64_t q = 0; q < cnt; ++q) {
+                const uint32_t col = (uint32_t)ptr_at(indices, indices_type, s0 + q);
+                const bool neg = val_at(data, data_type, s0 + q) < 0;
+                img.O[rec + 1 + (uint64_t)q] = (uint16_t)((neg ? 0x8000u : 0u) | col);
+            }
+            fill[b] += 1 + (uint64_t)cnt;
+        }
+    }
+    return RP_OK;
+}
+
+// the three buffers of an image: packed W/base/O, or generic Bp/Bj/values (values from the caller)
+void image_parts(const HostImage& img, const void* data, int32_t data_type, const void* src[3],
+                 int64_t bytes[3]) {
+    if (img.layout == RP_LAYOUT_PACKED) {
+        src[0] = img.W.data(); bytes[0] = 2 * (int64_t)img.W.size();
+        src[1] = img.base.data(); bytes[1] = 4 * (int64_t)img.base.size();
+        src[2] = img.O.data(); bytes[2] = 2 * (int64_t)img.O.size();
+    } else {
+        const int vs = dtype_size(data_type);
+        src[0] = img.Bp.data(); bytes[0] = 4 * (int64_t)img.Bp.size();
+        src[1] = img.Bj.data(); bytes[1] = 2 * (int64_t)img.Bj.size();
+        src[2] = data ? (const char*)data + (size_t)vs * (size_t)img.b0 : nullptr;
+        bytes[2] = (int64_t)vs * img.nnz;
+    }
+}
+
 }  // namespace
 
 // ==========================================================================================
@@ -894,142 +1018,73 @@ int rp_projector_create(int device, int64_t m, int64_t p, const void* indptr, in
                         int32_t data_type, int32_t layout, rp_projector** out) {
     if (!out) return fail(RP_ERR_INVALID, "NULL out");
     *out = nullptr;
-    if (m < 0 || p <= 0) return fail(RP_ERR_INVALID, "bad shape (%lld, %lld)", (long long)m, (long long)p);
-    if (!indptr || (indptr_type != RP_I32 && indptr_type != RP_I64) ||
-        (indices_type != RP_I32 && indices_type != RP_I64) ||
-        (data_type != RP_F32 && data_type != RP_F64))
-        return fail(RP_ERR_INVALID, "bad R arrays");
-    if (p > 32767) return fail(RP_ERR_UNSUPPORTED, "p=%lld > 32767 not supported by the GPU path", (long long)p);
-    const int64_t nnz = ptr_at(indptr, indptr_type, m) - ptr_at(indptr, indptr_type, 0);
-    const int64_t b0 = ptr_at(indptr, indptr_type, 0);
-    if (nnz < 0 || nnz >= ((int64_t)1 << 31) - 1) return fail(RP_ERR_UNSUPPORTED, "R nnz out of range");
-    if (nnz > 0 && (!indices || !data)) return fail(RP_ERR_INVALID, "NULL R indices/data");
-    if (m >= ((int64_t)1 << 31)) return fail(RP_ERR_UNSUPPORTED, "m >= 2^31");
-
-    // validate and detect the single-magnitude layout
-    double mag = 0.0;
-    bool single = p <= 8192 && nnz > 0;
-    for (int64_t q = 0; q < nnz; ++q) {
-        const int64_t col = ptr_at(indices, indices_type, b0 + q);
-        if (col < 0 || col >= p) return fail(RP_ERR_INVALID, "R column index %lld out of range", (long long)col);
-        if (single) {
-            const double v = val_at(data, data_type, b0 + q);
-            const double av = std::fabs(v);
-            if (q == 0) mag = av;
-            if (!(av == mag) || av == 0.0 || std::isnan(v)) single = false;
-        }
-    }
-    for (int64_t j = 0; j < m; ++j)
-        if (ptr_at(indptr, indptr_type, j + 1) < ptr_at(indptr, indptr_type, j))
-            return fail(RP_ERR_INVALID, "R indptr not monotone");
-    if (layout == RP_LAYOUT_PACKED && !single)
-        return fail(RP_ERR_UNSUPPORTED, "R does not qualify for the packed layout");
-    const bool packed = single && layout != RP_LAYOUT_GENERIC;
-
+    HostImage img;
+    int rc = build_image(m, p, indptr, indptr_type, indices, indices_type, data, data_type, layout, img);
+    if (rc) return rc;
     rp_projector* h = new (std::nothrow) rp_projector();
     if (!h) return fail(RP_ERR_NOMEM, "out of host memory");
     h->device = device;
     h->m = m;
     h->p = p;
-    h->nnz = nnz;
+    h->nnz = img.nnz;
     h->value_type = data_type;
+    h->layout = img.layout;
+    h->mag = img.mag;
+    h->bs = img.bs;
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) {
         delete h;
         return fail(RP_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e));
     }
-    int rc = RP_OK;
-    if (packed) {
-        h->layout = RP_LAYOUT_PACKED;
-        h->mag = mag;
-        // block shift: every block's overflow region must be addressable with 15 bits
-        int bs = 12;
-        std::vector<uint64_t> need;
-        for (;; --bs) {
-            const int64_t nb = (m + ((int64_t)1 << bs) - 1) >> bs;
-            need.assign((size_t)std::max<int64_t>(nb, 1), 0);
-            bool ok = true;
-            for (int64_t j = 0; j < m; ++j) {
-                const int64_t cnt = ptr_at(indptr, indptr_type, j + 1) - ptr_at(indptr, indptr_type, j);
-                if (cnt >= 2) need[(size_t)(j >> bs)] += 1 + (uint64_t)cnt;
-            }
-            for (uint64_t v : need) ok &= v <= 32767;
-            if (ok || bs == 0) break;
-        }
-        h->bs = bs;
-        const int64_t nb = (int64_t)need.size();
-        std::vector<uint32_t> base((size_t)nb);
-        uint64_t acc = 0;
-        for (int64_t b = 0; b < nb; ++b) {
-            base[(size_t)b] = (uint32_t)acc;
-            acc += need[(size_t)b];
-        }
-        if (acc >= ((uint64_t)1 << 32)) { delete h; return fail(RP_ERR_UNSUPPORTED, "overflow table too large"); }
-        std::vector<uint16_t> W((size_t)std::max<int64_t>(m, 1), 0);
-        std::vector<uint16_t> O((size_t)std::max<uint64_t>(acc, 1), 0);
-        std::vector<uint64_t> fill(base.begin(), base.end());
-        for (int64_t j = 0; j < m; ++j) {
-            const int64_t s = ptr_at(indptr, indptr_type, j), t = ptr_at(indptr, indptr_type, j + 1);
-            const int64_t cnt = t - s;
-            if (cnt == 1) {
-                const uint32_t col = (uint32_t)ptr_at(indices, indices_type, s);
-                const bool neg = val_at(data, data_type, s) < 0;
-                W[(size_t)j] = (uint16_t)(0x4000u | (neg ? 0x2000u : 0u) | col);
-            } else if (cnt >= 2) {
-                const size_t b = (size_t)(j >> bs);
-                const uint64_t rec = fill[b];
-                W[(size_t)j] = (uint16_t)(0x8000u | (uint32_t)(rec - base[b]));
-                O[rec] = (uint16_t)cnt;
-                for (int64_t q = 0; q < cnt; ++q) {
-                    const uint32_t col = (uint32_t)ptr_at(indices, indices_type, s + q);
-                    const bool neg = val_at(data, data_type, s + q) < 0;
-                    O[rec + 1 + (uint64_t)q] = (uint16_t)((neg ? 0x8000u : 0u) | col);
-                }
-                fill[b] += 1 + (uint64_t)cnt;
-            }
-        }
-        if ((rc = h->W.ensure(2 * W.size(), device)) || (rc = h->base.ensure(4 * base.size(), device)) ||
-            (rc = h->O.ensure(2 * O.size(), device))) {
-            delete h;
-            return rc;
-        }
-        h->W.bytes = 2 * (size_t)m;
-        h->base.bytes = 4 * base.size();
-        h->O.bytes = 2 * (size_t)acc;
-        e = hipMemcpy(h->W.p, W.data(), 2 * W.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(h->base.p, base.data(), 4 * base.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(h->O.p, O.data(), 2 * O.size(), hipMemcpyHostToDevice);
+    const void* src[3];
+    int64_t bytes[3];
+    image_parts(img, data, data_type, src, bytes);
+    DevBuf* dst[3];
+    if (img.layout == RP_LAYOUT_PACKED) {
+        dst[0] = &h->W; dst[1] = &h->base; dst[2] = &h->O;
     } else {
-        h->layout = RP_LAYOUT_GENERIC;
-        std::vector<int32_t> Bp((size_t)m + 1);
-        std::vector<uint16_t> Bj((size_t)std::max<int64_t>(nnz, 1));
-        for (int64_t j = 0; j <= m; ++j) Bp[(size_t)j] = (int32_t)(ptr_at(indptr, indptr_type, j) - b0);
-        for (int64_t q = 0; q < nnz; ++q) Bj[(size_t)q] = (uint16_t)ptr_at(indices, indices_type, b0 + q);
-        if ((rc = h->Bp.ensure(4 * Bp.size(), device)) || (rc = h->Bj.ensure(2 * Bj.size(), device))) {
+        dst[0] = &h->Bp; dst[1] = &h->Bj; dst[2] = data_type == RP_F64 ? &h->Bx64 : &h->Bx32;
+    }
+    for (int i = 0; i < 3; ++i) {
+        if ((rc = dst[i]->ensure((size_t)std::max<int64_t>(bytes[i], 2), device))) {
             delete h;
             return rc;
         }
-        h->Bp.bytes = 4 * Bp.size();
-        h->Bj.bytes = 2 * (size_t)nnz;
-        e = hipMemcpy(h->Bp.p, Bp.data(), 4 * Bp.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = hipMemcpy(h->Bj.p, Bj.data(), 2 * Bj.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess) {
-            DevBuf& dst = data_type == RP_F64 ? h->Bx64 : h->Bx32;
-            const size_t vs = (size_t)dtype_size(data_type);
-            if ((rc = dst.ensure(vs * (size_t)std::max<int64_t>(nnz, 1), device))) {
-                delete h;
-                return rc;
-            }
-            dst.bytes = vs * (size_t)nnz;
-            if (nnz > 0)
-                e = hipMemcpy(dst.p, (const char*)data + vs * (size_t)b0, vs * (size_t)nnz, hipMemcpyHostToDevice);
+        dst[i]->bytes = (size_t)bytes[i];
+        if (bytes[i] > 0) e = hipMemcpy(dst[i]->p, src[i], (size_t)bytes[i], hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            delete h;
+            return fail(RP_ERR_HIP, "R upload failed: %s", hipGetErrorString(e));
         }
-    }
-    if (e != hipSuccess) {
-        delete h;
-        return fail(RP_ERR_HIP, "R upload failed: %s", hipGetErrorString(e));
     }
     *out = h;
+    return RP_OK;
+}
+
+int rp_pack_r_host(int64_t m, int64_t p, const void* indptr, int32_t indptr_type, const void* indices,
+                   int32_t indices_type, const void* data, int32_t data_type, int32_t layout,
+                   rp_projector_info* info, void* buf0, void* buf1, void* buf2) {
+    if (!info) return fail(RP_ERR_INVALID, "NULL info");
+    HostImage img;
+    int rc = build_image(m, p, indptr, indptr_type, indices, indices_type, data, data_type, layout, img);
+    if (rc) return rc;
+    std::memset(info, 0, sizeof *info);
+    info->m = m;
+    info->p = p;
+    info->nnz = img.nnz;
+    info->layout = img.layout;
+    info->value_type = data_type;
+    info->magnitude = img.mag;
+    info->block_shift = img.bs;
+    info->n_buffers = 3;
+    const void* src[3];
+    int64_t bytes[3];
+    image_parts(img, data, data_type, src, bytes);
+    void* dst[3] = {buf0, buf1, buf2};
+    for (int i = 0; i < 3; ++i) {
+        info->buffer_bytes[i] = bytes[i];
+        if (dst[i] && bytes[i] > 0) std::memcpy(dst[i], src[i], (size_t)bytes[i]);
+    }
     return RP_OK;
 }
 

@@ -1,0 +1,97 @@
+"""The packed single-magnitude image of R (built on the host by rp_pack_r_host, the same code
+rp_projector_create uploads) decodes back to R exactly: rows, per-row order, signs."""
+import ctypes
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from randomprojection_amd import _native as nat
+from randomprojection_amd import srp_matrix as sm
+
+
+def pack(R, layout=nat.RP_LAYOUT_AUTO):
+    lib = nat.load()
+    R = sp.csr_matrix(R)
+    info = nat.ProjectorInfo()
+    args = (R.shape[0], R.shape[1], nat.ptr(R.indptr), nat.idx_code(R.indptr.dtype), nat.ptr(R.indices),
+            nat.idx_code(R.indices.dtype), nat.ptr(R.data), nat.val_code(R.data.dtype), layout, ctypes.byref(info))
+    nat.check(lib.rp_pack_r_host(*args, None, None, None))
+    bufs = [np.zeros(max(int(info.buffer_bytes[i]), 1), np.uint8) for i in range(3)]
+    nat.check(lib.rp_pack_r_host(*args, *[nat.ptr(b) for b in bufs]))
+    return info, bufs
+
+
+def decode_packed(info, bufs, dtype):
+    W = bufs[0][:info.buffer_bytes[0]].view(np.uint16)
+    base = bufs[1][:info.buffer_bytes[1]].view(np.uint32)
+    O = bufs[2][:info.buffer_bytes[2]].view(np.uint16)
+    mag = dtype(info.magnitude)
+    indptr, cols, vals = [0], [], []
+    for j, w in enumerate(W.tolist()):
+        if w & 0x8000:
+            rec = int(base[j >> info.block_shift]) + (w & 0x7FFF)
+            n = int(O[rec])
+            ent = O[rec + 1: rec + 1 + n].astype(np.int64)
+            cols.extend((ent & 0x7FFF).tolist())
+            vals.extend(np.where(ent & 0x8000, -mag, mag).tolist())
+        elif w & 0x4000:
+            cols.append(w & 0x1FFF)
+            vals.append(-mag if w & 0x2000 else mag)
+        else:
+            assert w == 0
+        indptr.append(len(cols))
+    return np.array(indptr), np.array(cols), np.array(vals, dtype=dtype)
+
+
+@pytest.mark.parametrize("m,p,dtype", [(100_000, 256, np.float32), (5000, 64, np.float64), (3000, 4096, np.float32)])
+def test_packed_roundtrip(m, p, dtype):
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123), dtype=dtype)
+    info, bufs = pack(R)
+    assert info.layout == nat.RP_LAYOUT_PACKED and info.nnz == R.nnz
+    assert info.magnitude == float(np.abs(R.data[0]))
+    ip, ix, vx = decode_packed(info, bufs, dtype)
+    assert np.array_equal(ip, R.indptr) and np.array_equal(ix, R.indices)
+    assert np.array_equal(vx.view(np.uint8), R.data.view(np.uint8))
+    assert info.buffer_bytes[0] == 2 * m                       # one u16 word per feature
+
+
+def test_block_shift_shrinks_for_dense_rows():
+    """Features with many entries overflow a 4096-feature block's 15-bit record offsets: the
+    packer picks a smaller block."""
+    rng = np.random.default_rng(0)
+    m, p = 8192, 4096
+    rows = [np.sort(rng.choice(p, size=40, replace=False)) for _ in range(m)]
+    indptr = np.arange(m + 1) * 40
+    R = sp.csr_matrix((np.where(rng.random(m * 40) < .5, -1.0, 1.0).astype(np.float32), np.concatenate(rows), indptr),
+                      shape=(m, p))
+    info, bufs = pack(R)
+    assert info.layout == nat.RP_LAYOUT_PACKED and info.block_shift < 12
+    ip, ix, vx = decode_packed(info, bufs, np.float32)
+    assert np.array_equal(ix, R.indices) and np.array_equal(vx, R.data)
+
+
+def test_generic_when_magnitudes_differ_or_forced():
+    R = sp.random(2000, 64, density=0.02, format="csr", dtype=np.float32, random_state=1)
+    info, bufs = pack(R)
+    assert info.layout == nat.RP_LAYOUT_GENERIC
+    Bp = bufs[0][:info.buffer_bytes[0]].view(np.int32)
+    Bj = bufs[1][:info.buffer_bytes[1]].view(np.uint16)
+    Bx = bufs[2][:info.buffer_bytes[2]].view(np.float32)
+    assert np.array_equal(Bp, R.indptr) and np.array_equal(Bj, R.indices) and np.array_equal(Bx, R.data)
+    R1 = sm.projection_operand(sm.sparse_random_matrix(64, 2000, random_state=123))
+    assert pack(R1, nat.RP_LAYOUT_GENERIC)[0].layout == nat.RP_LAYOUT_GENERIC
+    with pytest.raises(nat.RPError):
+        pack(R, nat.RP_LAYOUT_PACKED)
+
+
+def test_explicit_zero_entries_force_generic():
+    R = sm.projection_operand(sm.sparse_random_matrix(32, 1000, random_state=123))
+    R.data[3] = 0.0
+    assert pack(R)[0].layout == nat.RP_LAYOUT_GENERIC
+
+
+def test_invalid_r_rejected():
+    R = sp.csr_matrix((np.ones(2, np.float32), np.array([0, 70]), np.array([0, 1, 2])), shape=(2, 64))
+    with pytest.raises(nat.RPError, match="out of range"):
+        pack(R)
