@@ -33,6 +33,10 @@
  *      random_project_map_function (localmode/randomProjection.py:15-36) and
  *      SparseRandomProjection.transform (sklearn/random_projection.py:801-824).
  *
+ *  rp_libsvm_parse_device
+ *      spark.read.format("libsvm").load(path, numFeatures=m)  code/clustermode/randomProjection.py:71
+ *    libsvm text -> CSR on the GPU (Spark MLUtils.parseLibSVMRecord semantics).
+ *
  *  rp_synth_rows_device
  *      synthetic KDD2012-shaped rows generated in HBM (benchmarks; the reference downloads
  *      kdd12.tr with code/get_kdd2012_data.sh, not available offline).
@@ -159,6 +163,19 @@ int rp_synth_rows_device(int device, int64_t n_rows, int64_t m, double mean_extr
                          int32_t max_row_nnz, int32_t dist, double zipf_s, uint64_t seed,
                          void* indptr, int32_t indptr_type, int32_t* indices, float* data,
                          void* stream, int64_t* nnz);
+
+/* libsvm text -> CSR, both in device memory (replaces spark.read.format("libsvm").load(path,
+ * numFeatures=m), code/clustermode/randomProjection.py:71; Spark MLUtils.parseLibSVMRecord):
+ * lines trimmed, blank and '#' lines skipped, "label i:v i:v ..." split on single spaces,
+ * i 1-based -> 0-based, strictly ascending and < num_features, v parsed as double and stored as
+ * float32 (the partition function's astype(np.float32), clustermode:38), label kept as double.
+ * `text` must be 16-byte aligned. With indices == NULL only *n_rows and *nnz are computed;
+ * otherwise labels (cap_rows), indptr (cap_rows + 1), indices/data (cap_nnz) are filled.
+ * A malformed line gives RP_ERR_INVALID and *err_line = its 0-based line number. */
+int rp_libsvm_parse_device(int device, const char* text, int64_t n_bytes, int64_t num_features,
+                           double* labels, void* indptr, int32_t indptr_type, int32_t* indices,
+                           float* data, int64_t cap_rows, int64_t cap_nnz, void* stream,
+                           int64_t* n_rows, int64_t* nnz, int64_t* err_line);
 
 #ifdef __cplusplus
 }

@@ -22,7 +22,7 @@ EXPORTS = (
     "rp_projector_create_from_device", "rp_projector_destroy", "rp_pack_r_host",
     "rp_project_workspace_bytes", "rp_project_device",
     "rp_project_host_begin", "rp_result_fetch", "rp_result_free",
-    "rp_synth_rows_device",
+    "rp_synth_rows_device", "rp_libsvm_parse_device",
 )
 
 
@@ -93,6 +93,8 @@ def load(path: str = LIB_PATH):
         "rp_result_free": (ctypes.c_int, [vp]),
         "rp_synth_rows_device": (ctypes.c_int, [ctypes.c_int, i64, i64, dbl, i32, i32, dbl, ctypes.c_uint64,
                                                 vp, i32, vp, vp, vp, P(i64)]),
+        "rp_libsvm_parse_device": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, vp, vp, i32, vp, vp, i64, i64, vp,
+                                                  P(i64), P(i64), P(i64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -1,0 +1,93 @@
+// rp_common.h — host-side helpers shared by librp's translation units (error plumbing, device
+// buffers, dtype codes). Internal; the public interface is include/rp.h.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "../../include/rp.h"
+
+namespace rpd {
+
+// ------------------------------------------------------------------------------------------
+// error plumbing
+inline thread_local std::string g_err;
+
+inline int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+inline int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess)                                                                  \
+            return fail(RP_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
+                        __FILE__, __LINE__);                                                   \
+    } while (0)
+
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int device = -1;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(device);
+            (void)hipFree(p);
+            (void)hipSetDevice(cur);
+        }
+        p = nullptr;
+        bytes = 0;
+    }
+    int ensure(size_t n, int dev) {
+        if (n <= bytes && p) return RP_OK;
+        release();
+        device = dev;
+        size_t want = std::max<size_t>(n, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(RP_ERR_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        }
+        bytes = want;
+        return RP_OK;
+    }
+};
+
+
+inline int dtype_size(int t) {
+    switch (t) {
+        case RP_I32: case RP_F32: return 4;
+        case RP_I64: case RP_F64: return 8;
+        default: return 0;
+    }
+}
+
+template <typename I>
+inline int64_t idx_at(const void* a, int64_t i) { return (int64_t)((const I*)a)[i]; }
+inline int64_t ptr_at(const void* a, int t, int64_t i) {
+    return t == RP_I64 ? idx_at<int64_t>(a, i) : idx_at<int32_t>(a, i);
+}
+inline double val_at(const void* a, int t, int64_t i) {
+    return t == RP_F64 ? ((const double*)a)[i] : (double)((const float*)a)[i];
+}
+
+
+// inclusive prefix sum of n int64 values in place on `st` (defined in rp_spgemm.hip)
+int inclusive_scan_i64(int64_t* a, int64_t n, hipStream_t st, DevBuf& tmp, int device);
+
+}  // namespace rpd

@@ -34,31 +34,11 @@
 #include <vector>
 
 #include "../../include/rp.h"
+#include "rp_common.h"
+
+using namespace rpd;
 
 namespace {
-
-// ------------------------------------------------------------------------------------------
-// error plumbing
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...) {
-    char buf[1024];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    g_err = buf;
-    return code;
-}
-
-#define HIP_TRY(expr)                                                                          \
-    do {                                                                                       \
-        hipError_t e_ = (expr);                                                                \
-        if (e_ != hipSuccess)                                                                  \
-            return fail(RP_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
-                        __FILE__, __LINE__);                                                   \
-    } while (0)
 
 // ------------------------------------------------------------------------------------------
 // constants
@@ -629,37 +609,9 @@ __global__ void scan_add_kernel(int64_t* a, int64_t n, const int64_t* bsum_scann
 
 // ------------------------------------------------------------------------------------------
 // host-side structures
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-    int device = -1;
-    ~DevBuf() { release(); }
-    void release() {
-        if (p) {
-            int cur = 0;
-            (void)hipGetDevice(&cur);
-            (void)hipSetDevice(device);
-            (void)hipFree(p);
-            (void)hipSetDevice(cur);
-        }
-        p = nullptr;
-        bytes = 0;
-    }
-    int ensure(size_t n, int dev) {
-        if (n <= bytes && p) return RP_OK;
-        release();
-        device = dev;
-        size_t want = std::max<size_t>(n, 256);
-        hipError_t e = hipMalloc(&p, want);
-        if (e != hipSuccess) {
-            p = nullptr;
-            return fail(RP_ERR_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
-        }
-        bytes = want;
-        return RP_OK;
-    }
-};
+}  // namespace
 
+namespace rpd {
 int inclusive_scan_i64(int64_t* a, int64_t n, hipStream_t st, DevBuf& tmp, int device) {
     if (n <= 0) return RP_OK;
     const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
@@ -678,7 +630,7 @@ int inclusive_scan_i64(int64_t* a, int64_t n, hipStream_t st, DevBuf& tmp, int d
     return RP_OK;
 }
 
-}  // namespace
+}  // namespace rpd
 
 struct rp_projector {
     int device = 0;
@@ -705,23 +657,6 @@ struct rp_result {
 };
 
 namespace {
-
-int dtype_size(int t) {
-    switch (t) {
-        case RP_I32: case RP_F32: return 4;
-        case RP_I64: case RP_F64: return 8;
-        default: return 0;
-    }
-}
-
-template <typename I>
-int64_t idx_at(const void* a, int64_t i) { return (int64_t)((const I*)a)[i]; }
-int64_t ptr_at(const void* a, int t, int64_t i) {
-    return t == RP_I64 ? idx_at<int64_t>(a, i) : idx_at<int32_t>(a, i);
-}
-double val_at(const void* a, int t, int64_t i) {
-    return t == RP_F64 ? ((const double*)a)[i] : (double)((const float*)a)[i];
-}
 
 Caps choose_caps(int64_t n_rows, int64_t nnz_a, double prod_per_entry) {
     Caps c;

@@ -1,0 +1,141 @@
+"""libsvm ingest on the GPU.
+
+Replaces ``spark.read.format("libsvm").load(path, numFeatures=N_FEATURES)`` +
+``.withColumn("id", f.monotonically_increasing_id())`` (code/clustermode/randomProjection.py:71-72,
+code/localmode/randomProjection.py:92-96): text is read in newline-aligned chunks (a chunk plays
+the role of a Spark partition), copied to HBM and parsed by librp's ``rp_libsvm_parse_device``
+kernels into CSR (0-based ascending int32 indices, float32 values, float64 labels). Row ids follow
+``monotonically_increasing_id``: ``(chunk_index << 33) + row_in_chunk``.
+
+``project_libsvm`` chains ingest and projection on the device (boundary 3 of SURVEY.md §8(d):
+libsvm text -> projected CSR), so A never round-trips through the host.
+"""
+from __future__ import annotations
+
+import ctypes
+import mmap
+import os
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _native as nat
+
+__all__ = ["parse_device", "parse_bytes", "iter_chunks", "load_libsvm", "project_libsvm", "partition_ids"]
+
+DEFAULT_CHUNK = 256 << 20
+
+
+class LibsvmFormatError(ValueError):
+    def __init__(self, msg, line):
+        super().__init__(msg)
+        self.line = line
+
+
+def partition_ids(chunk_index: int, n_rows: int) -> np.ndarray:
+    """Spark ``monotonically_increasing_id``: partition id in the upper 31 bits, row in the lower 33."""
+    return (np.int64(chunk_index) << np.int64(33)) + np.arange(n_rows, dtype=np.int64)
+
+
+def parse_device(text, n_bytes: int, num_features: int, device: int = 0, stream: int = 0, indptr_dtype=None):
+    """Parse libsvm text already in device memory (a uint8 torch tensor, 16-byte aligned).
+    Returns torch tensors (labels f64, indptr, indices i32, data f32) on ``cuda:device``."""
+    import torch
+
+    lib = nat.load()
+    dev = torch.device("cuda", device)
+    rows, nnz, err = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(-1)
+    tp = ctypes.c_void_p(text.data_ptr())
+    nat.check(lib.rp_libsvm_parse_device(device, tp, n_bytes, num_features, None, None, nat.RP_I64, None, None,
+                                         0, 0, ctypes.c_void_p(stream), ctypes.byref(rows), ctypes.byref(nnz),
+                                         ctypes.byref(err)))
+    n, k = int(rows.value), int(nnz.value)
+    if indptr_dtype is None:
+        indptr_dtype = torch.int32 if k < 2**31 else torch.int64
+    labels = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    indptr = torch.empty(n + 1, dtype=indptr_dtype, device=dev)
+    indices = torch.empty(max(k, 1), dtype=torch.int32, device=dev)
+    data = torch.empty(max(k, 1), dtype=torch.float32, device=dev)
+    rc = lib.rp_libsvm_parse_device(device, tp, n_bytes, num_features, ctypes.c_void_p(labels.data_ptr()),
+                                    ctypes.c_void_p(indptr.data_ptr()),
+                                    nat.RP_I64 if indptr_dtype == torch.int64 else nat.RP_I32,
+                                    ctypes.c_void_p(indices.data_ptr()), ctypes.c_void_p(data.data_ptr()), n, k,
+                                    ctypes.c_void_p(stream), ctypes.byref(rows), ctypes.byref(nnz), ctypes.byref(err))
+    if rc == nat.RP_ERR_INVALID and err.value >= 0:
+        raise LibsvmFormatError(lib.rp_last_error().decode(), int(err.value))
+    nat.check(rc)
+    return labels[:n], indptr, indices[:k], data[:k]
+
+
+def _to_device(buf, device):
+    import torch
+
+    n = len(buf)
+    t = torch.empty((n + 15) // 16 * 16 + 16, dtype=torch.uint8, device=torch.device("cuda", device))
+    if n:
+        t[:n].copy_(torch.frombuffer(bytearray(buf) if not isinstance(buf, (bytearray, memoryview)) else buf,
+                                     dtype=torch.uint8))
+    return t, n
+
+
+def parse_bytes(buf, num_features: int, device: int = 0):
+    """Parse a bytes-like chunk of libsvm text -> (labels float64, scipy CSR float32)."""
+    t, n = _to_device(buf, device)
+    labels, indptr, indices, data = parse_device(t, n, num_features, device)
+    X = sp.csr_matrix((data.cpu().numpy(), indices.cpu().numpy(), indptr.cpu().numpy()),
+                      shape=(int(labels.numel()), num_features))
+    return labels.cpu().numpy(), X
+
+
+def iter_chunks(path: str, chunk_bytes: int = DEFAULT_CHUNK):
+    """Newline-aligned chunks of a file (memory-mapped, never loaded whole)."""
+    size = os.path.getsize(path)
+    if size == 0:
+        return
+    with open(path, "rb") as f, mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as mm:
+        start = 0
+        while start < size:
+            end = min(start + chunk_bytes, size)
+            if end < size:
+                nl = mm.rfind(b"\n", start, end)
+                if nl >= 0:
+                    end = nl + 1
+                else:  # one line longer than a chunk: extend to its end
+                    nxt = mm.find(b"\n", end)
+                    end = size if nxt < 0 else nxt + 1
+            yield memoryview(mm)[start:end].tobytes()
+            start = end
+
+
+def load_libsvm(path: str, num_features: int, chunk_bytes: int = DEFAULT_CHUNK, device: int = 0):
+    """Yield ``(ids, labels, X)`` per chunk — the rows of one Spark partition each."""
+    for ci, buf in enumerate(iter_chunks(path, chunk_bytes)):
+        labels, X = parse_bytes(buf, num_features, device)
+        yield partition_ids(ci, X.shape[0]), labels, X
+
+
+def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order: str = "sorted"):
+    """libsvm text -> GPU parse -> GPU projection -> host CSR, per chunk: yields
+    ``(ids, labels, C)`` with ``C`` = the chunk's rows of ``X @ R`` (scipy CSR, float32)."""
+    import torch
+
+    dev = projector.device
+    for ci, buf in enumerate(iter_chunks(path, chunk_bytes)):
+        t, n = _to_device(buf, dev)
+        labels, Ap, Aj, Ax = parse_device(t, n, projector.m, dev)
+        del t
+        rows = int(labels.numel())
+        cap = int(1.3 * Aj.numel() * projector.nnz / max(projector.m, 1)) + 1024
+        Cp = torch.empty(rows + 1, dtype=torch.int64, device=torch.device("cuda", dev))
+        Cj = torch.empty(cap, dtype=torch.int32, device=Cp.device)
+        Cx = torch.empty(cap, dtype=torch.float32, device=Cp.device)
+        try:
+            k = projector.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=order, nnz_a=int(Aj.numel()))
+        except nat.RPError as e:
+            if e.code != nat.RP_ERR_CAPACITY:
+                raise
+            Cj = torch.empty(e.nnz, dtype=torch.int32, device=Cp.device)
+            Cx = torch.empty(e.nnz, dtype=torch.float32, device=Cp.device)
+            k = projector.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=order, nnz_a=int(Aj.numel()))
+        C = sp.csr_matrix((Cx[:k].cpu().numpy(), Cj[:k].cpu().numpy(), Cp.cpu().numpy()), shape=(rows, projector.p))
+        yield partition_ids(ci, rows), labels.cpu().numpy(), C

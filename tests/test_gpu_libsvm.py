@@ -1,0 +1,92 @@
+"""GPU libsvm ingest vs the restated Spark parser (oracle/libsvm_ref.py), and the fused
+libsvm -> projection pipeline vs the oracle product."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import smmp
+from oracle.libsvm_ref import ParseError, parse_text
+from randomprojection_amd import Projector, srp_matrix as sm
+from randomprojection_amd.libsvm import LibsvmFormatError, parse_bytes, project_libsvm
+
+pytestmark = pytest.mark.gpu
+
+
+def random_text(rng, n, m, extras=True):
+    out = []
+    for i in range(n):
+        k = int(rng.integers(0, 25))
+        idx = np.sort(rng.choice(m, size=k, replace=False)) + 1
+        fmt = rng.integers(0, 6, size=k)
+        items = []
+        for j, f in zip(idx, fmt):
+            v = [f"{rng.integers(-9, 10)}", f"{rng.standard_normal():.6g}", f"{rng.random():.3e}",
+                 "1", f"{rng.integers(0, 1000)}.{rng.integers(0, 99)}", f".{rng.integers(1, 999)}"][f]
+            items.append(f"{j}:{v}")
+        sep = "  " if (extras and i % 7 == 0) else " "
+        label = ["1", "0", "-1", "+1", "0.5", "3e0"][i % 6]
+        line = label + (sep + sep.join(items) if items else "")
+        if extras and i % 11 == 0:
+            line = "  " + line + " \t"
+        out.append(line)
+        if extras and i % 13 == 0:
+            out.append("# comment line")
+        if extras and i % 17 == 0:
+            out.append("")
+    return ("\n".join(out) + ("\n" if n % 2 else "")).encode()
+
+
+def same(a, b):
+    return a.dtype == b.dtype and np.array_equal(np.asarray(a).view(np.uint8), np.asarray(b).view(np.uint8))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_parse_matches_oracle(seed):
+    rng = np.random.default_rng(seed)
+    m = 100_000
+    txt = random_text(rng, 3000 + seed * 1000, m)
+    lab, ip, ix, vx = parse_text(txt, m)
+    labels, X = parse_bytes(txt, m)
+    assert same(labels, lab) and np.array_equal(X.indptr, ip) and np.array_equal(X.indices, ix)
+    assert same(X.data, vx)
+
+
+def test_special_literals_and_edges():
+    txt = b"1 1:NaN 2:-Infinity 3:+Infinity 4:-0 5:1e21 6:100000000000000000000000 7:0.000001 8:1.\n\n#x\n2\n"
+    lab, ip, ix, vx = parse_text(txt, 10)
+    labels, X = parse_bytes(txt, 10)
+    assert same(labels, lab) and np.array_equal(X.indptr, ip) and np.array_equal(X.indices, ix)
+    assert same(X.data, vx)
+
+
+@pytest.mark.parametrize("line", ["1 0:1", "1 3:1 3:2", "1 101:1", "x 1:1", "1 a:1", "1 3:", "1 3:x", "1\t3:1"])
+def test_errors_report_line(line):
+    txt = ("2 1:1\n# c\n" + line + "\n1 1:1\n").encode()
+    with pytest.raises(ParseError) as ref:
+        parse_text(txt, 100)
+    with pytest.raises(LibsvmFormatError) as got:
+        parse_bytes(txt, 100)
+    assert got.value.line == ref.value.line == 2
+
+
+def test_project_libsvm_end_to_end(tmp_path):
+    rng = np.random.default_rng(5)
+    m, p = 200_000, 1024
+    txt = random_text(rng, 20_000, m, extras=False)
+    path = tmp_path / "train.libsvm"
+    path.write_bytes(txt)
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    P = Projector(R)
+    lab, ip, ix, vx = parse_text(txt, m)
+    A = sp.csr_matrix((vx, ix, ip), shape=(len(lab), m))
+    Cp, Cj, Cx, _, _ = smmp.matmat(A, R)
+    Cj_s, Cx_s = smmp.sorted_rows(Cp, Cj, Cx)
+    got_ids, got_lab, got_C = [], [], []
+    for ids, labels, C in project_libsvm(str(path), P, chunk_bytes=100_000):
+        got_ids.append(ids)
+        got_lab.append(labels)
+        got_C.append(C)
+    C = sp.vstack(got_C).tocsr()
+    assert same(np.concatenate(got_lab), lab)
+    assert np.array_equal(C.indptr, Cp) and np.array_equal(C.indices, Cj_s) and same(C.data, Cx_s)
+    assert all(int(i[0]) == (k << 33) for k, i in enumerate(got_ids))
