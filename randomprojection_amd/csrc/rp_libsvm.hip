@@ -177,6 +177,11 @@ __device__ double parse_double(const unsigned char* p, const unsigned char* end,
         mant /= 10;
         ++exp10;
     }
+    // Clinger's extended fast path: move surplus powers of ten into the mantissa while it stays exact
+    while (exp10 > 22 && mant <= (1ull << 53) / 10) {
+        mant *= 10;
+        --exp10;
+    }
     if (lost || mant > (1ull << 53) || exp10 < -22 || exp10 > 22) { *ok = 2; return 0.0; }
     const double pw[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
                            1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
