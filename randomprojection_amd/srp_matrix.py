@@ -193,3 +193,53 @@ KDD_M = 54_686_452
 KDD_P = 4096
 KDD_R_CSR_DIGEST = "51e3282ba4169367e3e8910370d9ef2593370781b90998a522d3f2c3842820c2"
 KDD_COMPONENTS_DIGEST = "723ac21a65d078f945cd57aed9bf53de5d2d68be0b6407b02fc02126fc594f46"
+
+
+# ------------------------------------------------------------------------------------------------
+# persistence: replaces the joblib pickle of the fitted estimator
+# (code/localmode/randomProjection.py:114-121 load-or-fit `srp_{p}.pkl`,
+#  code/clustermode/randomProjection.py:98 `joblib.dump(srp, "/tmp/srp.pkl")`).
+# Plain arrays in an .npz (no pickle, loadable with allow_pickle=False) plus the SURVEY digest.
+
+def save_components(path, components, *, random_state=None, density=None) -> str:
+    """Write ``components_`` (CSR, n_components x n_features) to ``path`` (.npz). Returns the digest
+    of the canonical (sorted) CSR, stored alongside and checked on load."""
+    C = sp.csr_matrix(components)
+    Cs = C.copy()
+    Cs.sort_indices()
+    digest = csr_digest(Cs.indptr, Cs.indices, Cs.data)
+    meta = np.array([C.shape[0], C.shape[1], -1 if random_state is None else int(random_state)], dtype=np.int64)
+    np.savez(path, indptr=C.indptr, indices=C.indices, data=C.data, meta=meta,
+             density=np.array([np.nan if density is None else float(density)]),
+             digest=np.frombuffer(digest.encode(), dtype=np.uint8))
+    return digest
+
+
+def load_components(path, verify: bool = True) -> sp.csr_matrix:
+    """Read a matrix written by ``save_components``; ``verify`` re-checks its digest."""
+    with np.load(path, allow_pickle=False) as z:
+        n, m = int(z["meta"][0]), int(z["meta"][1])
+        C = sp.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=(n, m))
+        digest = bytes(z["digest"]).decode()
+    if verify:
+        Cs = C.copy()
+        Cs.sort_indices()
+        if csr_digest(Cs.indptr, Cs.indices, Cs.data) != digest:
+            raise ValueError(f"{path}: digest mismatch (corrupt or edited projection matrix)")
+    return C
+
+
+def load_or_fit(path, n_components: int, n_features: int, random_state=123, density="auto", dtype=np.float32):
+    """localmode's load-or-fit cache (code/localmode/randomProjection.py:114-121) without pickles:
+    returns ``components_`` cast to ``dtype`` (the fit's ``astype(X.dtype)``)."""
+    import os
+
+    if os.path.exists(path):
+        C = load_components(path)
+        if C.shape != (n_components, n_features):
+            raise ValueError(f"{path}: cached shape {C.shape} != {(n_components, n_features)}")
+        return C.astype(dtype)
+    C = sparse_random_matrix(n_components, n_features, density=density, random_state=random_state).astype(dtype)
+    save_components(path, C, random_state=random_state if isinstance(random_state, (int, np.integer)) else None,
+                    density=check_density(density, n_features))
+    return C

@@ -1,0 +1,47 @@
+"""Output egress: rows in the reference's tuple form and the Spark-layout Parquet writer."""
+import json
+
+import numpy as np
+import scipy.sparse as sp
+
+from randomprojection_amd.egress import SPARK_SCHEMA_JSON, read_parquet, rows, write_parquet
+
+
+def _C(n=500, p=4096, seed=0):
+    C = sp.random(n, p, density=0.002, format="csr", dtype=np.float32, random_state=seed)
+    C.indices = C.indices[::-1].copy() if False else C.indices
+    return C
+
+
+def test_rows_sorted_f64():
+    C = _C()
+    Cu = sp.csr_matrix((C.data[::-1].copy(), C.indices.copy(), C.indptr.copy()), shape=C.shape)
+    # reverse each row's storage order (the scipy raw order is unsorted)
+    for i in range(Cu.shape[0]):
+        s, e = Cu.indptr[i], Cu.indptr[i + 1]
+        Cu.indices[s:e] = C.indices[s:e][::-1]
+        Cu.data[s:e] = C.data[s:e][::-1]
+    out = list(rows(np.arange(C.shape[0]), np.ones(C.shape[0]), Cu))
+    for i, (rid, lab, v) in enumerate(out):
+        s, e = C.indptr[i], C.indptr[i + 1]
+        assert rid == i and v.size == 4096 and np.array_equal(v.indices, C.indices[s:e])
+        assert v.values.dtype == np.float64 and np.array_equal(v.values, C.data[s:e].astype(np.float64))
+
+
+def test_parquet_roundtrip_and_spark_schema(tmp_path):
+    import pyarrow.parquet as pq
+
+    C = _C(seed=3)
+    ids = (np.int64(2) << 33) + np.arange(C.shape[0])
+    labels = (np.arange(C.shape[0]) % 2).astype(np.float64)
+    path = tmp_path / "part-00000.parquet"
+    write_parquet(str(path), ids, labels, C)
+    rid, rlab, RC = read_parquet(str(path))
+    assert np.array_equal(rid, ids) and np.array_equal(rlab, labels.astype(np.float32))
+    assert np.array_equal(RC.indptr, C.indptr) and np.array_equal(RC.indices, C.indices)
+    assert np.array_equal(RC.data, C.data.astype(np.float64))
+    meta = pq.read_schema(str(path)).metadata[b"org.apache.spark.sql.parquet.row.metadata"]
+    sch = json.loads(meta)
+    assert sch == json.loads(SPARK_SCHEMA_JSON)
+    assert [f["name"] for f in sch["fields"]] == ["id", "label", "features"]
+    assert sch["fields"][2]["type"]["class"] == "org.apache.spark.ml.linalg.VectorUDT"

@@ -76,3 +76,22 @@ def test_full_kdd_digest():
     assert sm.csr_digest(R.indptr, R.indices, R.data) == sm.KDD_R_CSR_DIGEST
     c32.sort_indices()
     assert sm.csr_digest(c32.indptr, c32.indices, c32.data) == sm.KDD_COMPONENTS_DIGEST
+
+
+def test_npz_persistence_roundtrip(tmp_path):
+    path = tmp_path / "srp_256.npz"
+    C = sm.load_or_fit(str(path), 256, 100_000)          # fits and saves
+    assert path.exists()
+    C2 = sm.load_or_fit(str(path), 256, 100_000)         # loads (no pickle) and verifies the digest
+    assert np.array_equal(C.indices, C2.indices) and same_bits(C.data, C2.data)
+    ref = _sk(100_000, 256, dtype=np.float32)
+    assert np.array_equal(C2.indices, ref.indices) and same_bits(C2.data, ref.data)
+    z = dict(np.load(path, allow_pickle=False))
+    z["data"] = z["data"].copy()
+    z["data"][0] *= -1
+    np.savez(path, **z)
+    with pytest.raises(ValueError, match="digest"):
+        sm.load_components(str(path))
+    sm.save_components(str(path), C)
+    with pytest.raises(ValueError, match="shape"):
+        sm.load_or_fit(str(path), 128, 100_000)
