@@ -1,0 +1,20 @@
+#!/bin/bash
+# Profiling session: full-size bench (configs[1]) + rocprofv3 kernel trace/stats + separate PMC passes.
+# Every GPU step has its own time limit; the first failure ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG="${TAG:-r01}"
+BA="${BENCH_ARGS:---steps 10 --warmup 3}"
+PA="${PROF_ARGS:---steps 5 --warmup 2 --no-cpu-baseline}"
+run() { echo "== $*" >&2; "$@"; }
+run timeout -k 10 600 python -u bench.py $BA > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { tail -20 gpurun_out/bench_full.err; exit 4; }
+cat gpurun_out/bench_full.json
+run timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_${TAG}_trace -o trace -- python3 bench.py $PA > gpurun_out/prof_trace.log 2>&1 || { tail -20 gpurun_out/prof_trace.log; exit 5; }
+for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum"; do
+  name=$(echo $pmc | tr ' ' '_')
+  run timeout -s KILL 300 rocprofv3 --pmc $pmc -T --output-format csv -d gpurun_out/prof_${TAG}_pmc_$name -o pmc -- python3 bench.py $PA > gpurun_out/prof_pmc_$name.log 2>&1 || { tail -20 gpurun_out/prof_pmc_$name.log; exit 6; }
+done
+find gpurun_out -name "*stats*.csv" | head
+exit 0

@@ -217,14 +217,22 @@ def test_errors_are_loud():
 
 
 def test_index64_inputs_follow_scipy_dtype_rule():
+    """scipy picks int64 output indices for int64 inputs, then the container's constructor decides:
+    csr_matrix downcasts indices that fit (int32), csr_array keeps int64. Same here."""
     rng = np.random.default_rng(3)
     m = 20_000
     R = sm.projection_operand(sm.sparse_random_matrix(128, m, random_state=123))
     A = kdd_like(rng, 500, m, values="normal")
-    A64 = sp.csr_matrix((A.data, A.indices.astype(np.int64), A.indptr.astype(np.int64)), shape=A.shape)
-    C, Cr = Projector(R).matmul(A64), A64 @ R
-    assert C.indices.dtype == Cr.indices.dtype == np.int64
-    assert_same_csr(C, Cr.indptr, Cr.indices, Cr.data)
+    P = Projector(R)
+    for cls, want in ((sp.csr_array, np.int64), (sp.csr_matrix, np.int32)):
+        A64 = cls((A.data, A.indices.astype(np.int64), A.indptr.astype(np.int64)), shape=A.shape)
+        if cls is sp.csr_matrix:
+            A64.indices = A64.indices.astype(np.int64)
+            A64.indptr = A64.indptr.astype(np.int64)
+        C, Cr = P.matmul(A64), A64 @ R
+        assert type(C) is type(Cr)
+        assert C.indices.dtype == Cr.indices.dtype == want and C.indptr.dtype == Cr.indptr.dtype
+        assert_same_csr(C, Cr.indptr, Cr.indices, Cr.data)
 
 
 @pytest.mark.slow
