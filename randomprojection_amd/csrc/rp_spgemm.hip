@@ -167,37 +167,55 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wsum
     return base + inc - v;
 }
 
-// decoupled look-back (thread 0 only): publish this tile's aggregate, sum predecessors' aggregates
-// until an inclusive prefix is found, publish the inclusive prefix. Each state is one 8-byte
-// granule {flag, value} written and read with relaxed agent-scope atomics (sc1), so no separate
-// payload needs ordering (MI355X_MICROARCH.md, Workgroup dispatch: granule hand-off).
-__device__ unsigned long long lookback(unsigned long long* states, unsigned int tile,
-                                       unsigned long long agg, Workspace* ws) {
+// decoupled look-back, executed by wave 0 of the workgroup (all 64 lanes): publish this tile's
+// aggregate, then read the states of 64 predecessors per poll (lane l reads tile - 1 - l - 64k),
+// summing aggregates up to the nearest inclusive prefix; publish the inclusive prefix. Each state
+// is one 8-byte granule {flag, value} written and read with relaxed agent-scope atomics (sc1), so
+// no separate payload needs ordering (MI355X_MICROARCH.md, Workgroup dispatch: granule hand-off).
+// Waits are bounded (kSpinLimit polls with s_sleep); a timeout sets ws->error.
+__device__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__device__ unsigned long long lookback_wave(unsigned long long* states, unsigned int tile,
+                                            unsigned long long agg, Workspace* ws) {
+    const int lane = threadIdx.x & 63;
     if (tile == 0) {
-        __hip_atomic_store(&states[0], kFlagP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0)
+            __hip_atomic_store(&states[0], kFlagP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    __hip_atomic_store(&states[tile], kFlagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+        __hip_atomic_store(&states[tile], kFlagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long excl = 0;
-    long i = (long)tile - 1;
+    long base = (long)tile - 1;  // nearest predecessor not yet summed
     long spins = 0;
-    while (i >= 0) {
-        unsigned long long s =
-            __hip_atomic_load(&states[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (s == 0) {
-            if (++spins > kSpinLimit) {
-                atomicOr(&ws->error, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
+    while (true) {
+        const long idx = base - lane;
+        unsigned long long st = idx >= 0 ? __hip_atomic_load(&states[idx], __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)
+                                         : kFlagP;  // before tile 0: prefix 0
+        const unsigned long long ready = __ballot(st != 0);
+        const unsigned long long pmask = __ballot((st & ~kValMask) == kFlagP);
+        const int first_p = pmask ? __builtin_ctzll(pmask) : 64;
+        const unsigned long long need = first_p >= 63 ? ~0ull : ((2ull << first_p) - 1);
+        if ((ready & need) == need) {
+            excl += wave_sum_u64(lane <= first_p ? (st & kValMask) : 0ull);
+            if (first_p < 64) break;
+            base -= 64;
             continue;
         }
-        excl += s & kValMask;
-        if ((s & ~kValMask) == kFlagP) break;
-        --i;
+        if (++spins > kSpinLimit) {
+            if (lane == 0) atomicOr(&ws->error, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
-    __hip_atomic_store(&states[tile], kFlagP | (excl + agg), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0)
+        __hip_atomic_store(&states[tile], kFlagP | (excl + agg), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     return excl;
 }
 
@@ -419,7 +437,10 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 // stage 3: tile offsets, look-back, staged coalesced write
                 uint32_t tile_c;
                 const uint32_t o_r = block_excl_scan(tid < nrows ? c : 0u, s_wsum, &tile_c);
-                if (tid == 0) s_off = lookback(states, tile, tile_c, ws);
+                if (tid < 64) {
+                    const unsigned long long g = lookback_wave(states, tile, tile_c, ws);
+                    if (tid == 0) s_off = g;
+                }
                 __syncthreads();
                 const unsigned long long G = s_off;
                 const bool write = G + tile_c <= capacity;
@@ -481,7 +502,10 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                                   Cx, false, order);
     uint32_t tile_c;
     (void)block_excl_scan(tid < nrows ? s_rowc[tid] : 0u, s_wsum, &tile_c);
-    if (tid == 0) s_off = lookback(states, tile, tile_c, ws);
+    if (tid < 64) {
+        const unsigned long long g = lookback_wave(states, tile, tile_c, ws);
+        if (tid == 0) s_off = g;
+    }
     __syncthreads();
     const unsigned long long G = s_off;
     const bool write = G + tile_c <= capacity;
