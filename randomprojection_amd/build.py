@@ -24,15 +24,21 @@ def needs_build() -> bool:
     return any(os.path.getmtime(s) > t for s in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if force or needs_build():
-        cmd = [HIPCC, *FLAGS, "-o", OUT + ".tmp", *SRC]
+DIAG_OUT = os.path.join(HERE, "librp_diag.so")
+
+
+def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
+    """librp.so; ``diag=True`` builds librp_diag.so instead (in-kernel stage stamps, -DRP_STAMPS),
+    used only by scripts/stage_stamps.py, never by the package."""
+    out = DIAG_OUT if diag else OUT
+    if force or diag or needs_build():
+        cmd = [HIPCC, *FLAGS, *(["-DRP_STAMPS"] if diag else []), "-o", out + ".tmp", *SRC]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-        os.replace(OUT + ".tmp", OUT)
-    return OUT
+        os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))

@@ -52,6 +52,21 @@ constexpr uint64_t kFlagP = 2ull << 62;   // tile inclusive prefix published
 constexpr uint64_t kValMask = (1ull << 62) - 1;
 constexpr long kSpinLimit = 1l << 27;     // bounded waits (with s_sleep): seconds, never minutes
 
+// Diagnostic builds (-DRP_STAMPS, librp_diag.so only): thread 0 of each tile records
+// s_memrealtime (100 MHz) at stage boundaries into g_stamps[tile * 8 + k]. Never in librp.so.
+#ifdef RP_STAMPS
+__device__ unsigned long long* g_stamps;
+#define STAMP(k)                                                                                  \
+    do {                                                                                          \
+        if (threadIdx.x == 0 && g_stamps)                                                         \
+            g_stamps[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
+
 struct Workspace {              // device memory header; tile states follow at +64 bytes
     unsigned int tile_counter;
     unsigned int error;
@@ -334,6 +349,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     __syncthreads();
     const unsigned int tile = s_tile;
     if (tile >= n_tiles) return;  // uniform
+    STAMP(0);
 
     const int64_t row0 = (int64_t)tile * caps.rpt;
     const int nrows = (int)std::min<int64_t>(caps.rpt, n_rows - row0);
@@ -375,6 +391,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
             }
         }
         __syncthreads();
+        STAMP(1);
         // stage 1b: exclusive scan of counts (contiguous chunk per thread)
         const uint32_t per = (ne + kBlock - 1) / kBlock;
         const uint32_t c0 = std::min<uint32_t>(tid * per, ne), c1 = std::min<uint32_t>(c0 + per, ne);
@@ -390,6 +407,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
         if (tid == 0) s_eoff[ne] = total;
         P_t = total;
         __syncthreads();
+        STAMP(2);
         heavy = P_t > (uint32_t)caps.cap_p;  // uniform
         if (!heavy) {
             // stage 1c: products into LDS, in (entry, R-entry) order
@@ -408,6 +426,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 }
             }
             __syncthreads();
+            STAMP(3);
             // stage 2: per-row ordered accumulation, list in place at the front of the row's slots
             uint32_t c = 0, n = 0, s = 0;
             if (tid < nrows) {
@@ -433,6 +452,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 }
             }
             __syncthreads();
+            STAMP(4);
             if (!s_heavy) {
                 // stage 3: tile offsets, look-back, staged coalesced write
                 uint32_t tile_c;
@@ -442,6 +462,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     if (tid == 0) s_off = g;
                 }
                 __syncthreads();
+                STAMP(5);
                 const unsigned long long G = s_off;
                 const bool write = G + tile_c <= capacity;
                 if (tid < nrows) {
@@ -492,12 +513,14 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                         Cx[G + q] = s_ov[q];
                     }
                 }
+                STAMP(6);
                 return;
             }
             heavy = true;
         }
     }
     // ---- exact sequential path (uniform branch)
+    STAMP(7);
     heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, 0, 0, Cp, Cj,
                                   Cx, false, order);
     uint32_t tile_c;
@@ -956,6 +979,13 @@ void image_parts(const HostImage& img, const void* data, int32_t data_type, cons
 // ==========================================================================================
 // C-ABI
 extern "C" {
+
+#ifdef RP_STAMPS
+int rp_debug_stamps(void* dev_buf) {
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_buf, sizeof(void*)));
+    return RP_OK;
+}
+#endif
 
 const char* rp_last_error(void) { return g_err.c_str(); }
 const char* rp_version(void) { return "rp-mi355x 0.1 (gfx950)"; }

@@ -1,0 +1,66 @@
+"""Where does a tile's time go? Runs the diagnostic build (librp_diag.so, -DRP_STAMPS) on synthetic
+KDD-shaped rows and prints per-stage durations from in-kernel s_memrealtime stamps (100 MHz).
+Diagnostic only: stamps perturb timing; read the SHARES, not the absolute kernel time.
+
+    python scripts/stage_stamps.py [--rows N] [--dist uniform|powerlaw]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=20_000_000)
+    ap.add_argument("--dist", default="uniform")
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stamps.json"))
+    args = ap.parse_args()
+
+    from randomprojection_amd import _native as nat
+    lib = nat.load(os.path.join(ROOT, "randomprojection_amd", "librp_diag.so"))
+    lib.rp_debug_stamps.argtypes = [ctypes.c_void_p]
+    import torch
+    from randomprojection_amd import Projector, srp_matrix as sm, synth
+
+    R = sm.projection_operand(sm.sparse_random_matrix(4096, sm.KDD_M, random_state=123))
+    P = Projector(R)
+    Ap, Aj, Ax = synth.kdd_rows_device(args.rows, sm.KDD_M, seed=7, dist=args.dist)
+    n_tiles = (args.rows + 255) // 256
+    stamps = torch.zeros(n_tiles * 8, dtype=torch.int64, device="cuda")
+    cap = int(1.3 * Aj.numel() * P.nnz / P.m) + 1024
+    Cp = torch.empty(args.rows + 1, dtype=torch.int32, device="cuda")
+    Cj = torch.empty(cap, dtype=torch.int32, device="cuda")
+    Cx = torch.empty(cap, dtype=torch.float32, device="cuda")
+    nat.check(lib.rp_debug_stamps(ctypes.c_void_p(0)))
+    P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, nnz_a=Aj.numel())          # warm, no stamps
+    nat.check(lib.rp_debug_stamps(ctypes.c_void_p(stamps.data_ptr())))
+    P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, nnz_a=Aj.numel())
+    torch.cuda.synchronize()
+    st = stamps.view(n_tiles, 8).cpu().numpy().astype(np.int64)
+    t0 = st[:, 0].min()
+    names = ["gather(1a)", "scan(1b)", "products(1c)", "accumulate(2)", "scan+lookback(3a)", "write(3b)"]
+    res = {"tiles": int(n_tiles), "heavy_tiles": int((st[:, 7] > 0).sum())}
+    ok = st[:, 6] > 0
+    for k, nm in enumerate(names):
+        d = (st[ok, k + 1] - st[ok, k]) * 10.0 / 1000.0  # 100 MHz ticks -> us
+        res[nm] = {"median_us": float(np.median(d)), "p90_us": float(np.percentile(d, 90)), "mean_us": float(d.mean())}
+    life = (st[ok, 6] - st[ok, 0]) * 10.0 / 1000.0
+    res["tile_life_us"] = {"median": float(np.median(life)), "p90": float(np.percentile(life, 90))}
+    span = (st[ok, 6].max() - t0) * 10.0 / 1e6
+    res["kernel_span_ms"] = float(span)
+    # mean concurrency = sum of lifetimes / span
+    res["mean_tiles_in_flight"] = float(life.sum() / 1000.0 / span)
+    print(json.dumps(res, indent=1))
+    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    json.dump(res, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
