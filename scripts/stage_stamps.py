@@ -23,10 +23,12 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stamps.json"))
     args = ap.parse_args()
 
+    import torch
+
+    torch.cuda.set_device(0)   # initialise torch's HIP context before librp touches the device
     from randomprojection_amd import _native as nat
     lib = nat.load(os.path.join(ROOT, "randomprojection_amd", "librp_diag.so"))
     lib.rp_debug_stamps.argtypes = [ctypes.c_void_p]
-    import torch
     from randomprojection_amd import Projector, srp_matrix as sm, synth
 
     R = sm.projection_operand(sm.sparse_random_matrix(4096, sm.KDD_M, random_state=123))
