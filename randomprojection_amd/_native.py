@@ -73,6 +73,14 @@ def load(path: str = LIB_PATH):
         raise NativeUnavailable(
             f"{path} is missing: build it with `python -m randomprojection_amd.build` "
             "(hipcc --offload-arch=gfx950); there is no CPU fallback")
+    # torch wheels bundle their own libamdhip64.so.7 (+ HSA runtime). If librp pulled in
+    # /opt/rocm's copy first, torch's later CUDA init would fail ("No HIP GPUs are available").
+    # Importing torch first makes librp bind to the runtime already in the process (same SONAME),
+    # so exactly one HIP runtime exists whichever side touches the GPU first.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # noqa: BLE001 - torch is optional for the host drop-ins
+        pass
     lib = ctypes.CDLL(path)
     vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
     P = ctypes.POINTER
