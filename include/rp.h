@@ -63,7 +63,7 @@ typedef enum {
 typedef enum { RP_I32 = 1, RP_I64 = 2, RP_F32 = 3, RP_F64 = 4 } rp_dtype;
 
 typedef enum {
-    RP_LAYOUT_AUTO = 0,      /* packed when R has one magnitude and p <= 8192, else generic */
+    RP_LAYOUT_AUTO = 0,      /* packed when R has one magnitude and p <= 16384, else generic */
     RP_LAYOUT_GENERIC = 1,   /* CSR (int32 indptr, uint16 columns, values) */
     RP_LAYOUT_PACKED = 2     /* require the packed layout; RP_ERR_UNSUPPORTED if R does not fit */
 } rp_layout;
@@ -81,9 +81,9 @@ typedef struct {
     int32_t layout;          /* RP_LAYOUT_GENERIC or RP_LAYOUT_PACKED */
     int32_t value_type;      /* RP_F32 / RP_F64: dtype R was given in */
     double magnitude;        /* packed: |value| of every entry; generic: 0 */
-    int32_t block_shift;     /* packed: features per overflow block = 1 << block_shift */
+    int32_t block_shift;     /* reserved (0) */
     int32_t n_buffers;       /* device buffers making up the image (<= 4) */
-    int64_t buffer_bytes[4]; /* packed: W(u16[m]), block base(u32), records(u16); generic: Bp, Bj, Bx */
+    int64_t buffer_bytes[4]; /* packed: W (u64[m]), long-row records (u16), -; generic: Bp, Bj, Bx */
 } rp_projector_info;
 
 /* A CSR operand. Host or device memory depending on the call. */

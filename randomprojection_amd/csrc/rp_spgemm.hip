@@ -45,7 +45,7 @@ namespace {
 constexpr int kBlock = 256;          // threads per workgroup = max rows per tile
 constexpr int kMaxE = 16;            // strided A entries held per thread in stage 1
 constexpr int kCapAMax = kBlock * kMaxE;  // 4096 entries per tile at most on the fast path
-constexpr int kRowProdMax = 192;     // a row with more products goes to the exact dense path
+constexpr int kRowProdMax = 1024;    // a row with more products goes to the exact dense path
 
 constexpr uint64_t kFlagA = 1ull << 62;   // tile aggregate published
 constexpr uint64_t kFlagP = 2ull << 62;   // tile inclusive prefix published
@@ -77,18 +77,20 @@ struct Workspace {              // device memory header; tile states follow at +
 // ------------------------------------------------------------------------------------------
 // R layouts
 //
-// Packed (single magnitude, p <= 8192): one 16-bit word per feature j:
-//   0                         : no entries
-//   01 s ccccccccccccc        : one entry, sign s, column c (13 bits)
-//   1  ooooooooooooooo        : >= 2 entries, record at O[base[j >> bs] + o]:
-//                               O[rec] = count n, O[rec+1..rec+n] = (sign << 15) | column
+// Packed (single magnitude, p <= 16384): one 64-bit word per feature j
+//   bits 61..63 = n, the feature's entry count, if n <= 4: entry t in bits [15t, 15t + 15) as
+//                 (sign << 14) | column (14 bits), in R's storage order;
+//   bits 61..63 = 7: more than 4 entries, bits 0..60 = offset of a record in O (u16):
+//                 O[rec] = n, O[rec+1..rec+n] = (sign << 15) | column.
+// One gather serves the whole R row for 99.97% of KDD2012 features (every L2 miss costs a whole
+// line whatever its width, so the wide word is free and no dependent record load is needed).
 // Value of an entry = sign ? -mag : mag, so x * value == x * Bx bitwise (IEEE negation symmetry).
 struct PackedR {
-    const uint16_t* W;
-    const uint32_t* base;
+    const uint64_t* W;
     const uint16_t* O;
-    int bs;
 };
+constexpr uint64_t kOvf = 7ull << 61;
+constexpr uint64_t kLow61 = (1ull << 61) - 1;
 // Generic CSR (any values): Bp int32 (m + 1), Bj uint16, Bx in the compute type.
 template <typename T>
 struct GenericR {
@@ -98,24 +100,25 @@ struct GenericR {
 };
 
 // descriptor of the R row of one A entry, produced in stage 1
-//   packed : d = single entry (bit 31 clear), or 0x80000000 | (record offset + 1) (first entry)
+//   packed : d = the word itself, or kOvf | (record offset + 1) (first entry) for long rows
 //   generic: d = Bp[j]
 template <typename T>
-__device__ __forceinline__ uint32_t r_describe(const PackedR& R, int32_t j, uint32_t& cnt) {
-    uint32_t w = R.W[j];
-    if (w & 0x8000u) {
-        uint32_t rec = R.base[j >> R.bs] + (w & 0x7fffu);
+__device__ __forceinline__ uint64_t r_describe(const PackedR& R, int32_t j, uint32_t& cnt) {
+    const uint64_t w = R.W[j];
+    const uint32_t n = (uint32_t)(w >> 61);
+    if (n == 7) {
+        const uint64_t rec = w & kLow61;
         cnt = R.O[rec];
-        return 0x80000000u | (rec + 1);
+        return kOvf | (rec + 1);
     }
-    cnt = (w >> 14) & 1u;
-    return w & 0x3fffu;
+    cnt = n;
+    return w;
 }
 template <typename T>
-__device__ __forceinline__ uint32_t r_describe(const GenericR<T>& R, int32_t j, uint32_t& cnt) {
+__device__ __forceinline__ uint64_t r_describe(const GenericR<T>& R, int32_t j, uint32_t& cnt) {
     int32_t b0 = R.Bp[j];
     cnt = (uint32_t)(R.Bp[j + 1] - b0);
-    return (uint32_t)b0;
+    return (uint64_t)(uint32_t)b0;
 }
 
 template <typename T>
@@ -133,23 +136,24 @@ __device__ __forceinline__ double tadd<double>(double a, double b) { return __da
 
 // t-th product (column, x * value) of an entry described by d
 template <typename T>
-__device__ __forceinline__ void r_product(const PackedR& R, T mag, uint32_t d, uint32_t t, T x,
+__device__ __forceinline__ void r_product(const PackedR& R, T mag, uint64_t d, uint32_t t, T x,
                                           uint32_t& col, T& v) {
-    uint32_t e;
-    if (d & 0x80000000u) {
-        e = R.O[(d & 0x7fffffffu) + t];
+    if ((d >> 61) == 7) {
+        const uint32_t e = R.O[(d & kLow61) + t];
         col = e & 0x7fffu;
         v = tmul<T>(x, (e & 0x8000u) ? -mag : mag);
     } else {
-        col = d & 0x1fffu;
-        v = tmul<T>(x, (d & 0x2000u) ? -mag : mag);
+        const uint32_t e = (uint32_t)(d >> (15 * t)) & 0x7fffu;
+        col = e & 0x3fffu;
+        v = tmul<T>(x, (e & 0x4000u) ? -mag : mag);
     }
 }
 template <typename T>
-__device__ __forceinline__ void r_product(const GenericR<T>& R, T, uint32_t d, uint32_t t, T x,
+__device__ __forceinline__ void r_product(const GenericR<T>& R, T, uint64_t d, uint32_t t, T x,
                                           uint32_t& col, T& v) {
-    col = R.Bj[d + t];
-    v = tmul<T>(x, R.Bx[d + t]);
+    const uint32_t b0 = (uint32_t)d;
+    col = R.Bj[b0 + t];
+    v = tmul<T>(x, R.Bx[b0 + t]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -260,7 +264,7 @@ __device__ void heavy_tile(const RL& R, T mag, const IP* __restrict__ Ap,
                 const int32_t j = Aj[jj];
                 const T x = Ax[jj];
                 uint32_t cnt;
-                const uint32_t d = r_describe<T>(R, j, cnt);
+                const uint64_t d = r_describe<T>(R, j, cnt);
                 for (uint32_t t = 0; t < cnt; ++t) {
                     uint32_t k;
                     T v;
@@ -321,9 +325,48 @@ __device__ void heavy_tile(const RL& R, T mag, const IP* __restrict__ Ap,
 // the fused kernel
 struct Caps {
     int cap_a;   // A entries per tile on the fast path (<= kCapAMax)
-    int cap_p;   // products per tile on the fast path
+    int cap_p;   // products per tile on the fast path (<= 65535)
     int rpt;     // rows per tile (<= kBlock)
 };
+
+// Dynamic-LDS carve-up of a tile (host sizes it, device uses it; all offsets 16-byte aligned):
+//   X  : eoff[cap_a + 1] (u32, stage 1)            | staged output cols (u16) + vals (T) (stage 3)
+//   P  : pv[cap_p] (T), pk[cap_p] (u16)             products, then leaders' sums in place
+//   U  : erow[cap_a] (u8, stage 1)                  | flag/rank[cap_p + 1] (u16, stages 2-3)
+//   PR : prow[cap_p] (u8)                           row of each product
+struct TileLayout {
+    size_t x, p, u, pr, total;
+    __host__ __device__ TileLayout(const Caps& c, size_t vs) {
+        auto al = [](size_t v) { return (v + 15) & ~size_t(15); };
+        const size_t xb = std::max<size_t>(4 * (size_t)(c.cap_a + 1), (2 + vs) * (size_t)c.cap_p + 16);
+        x = 0;
+        p = al(xb);
+        u = p + al((2 + vs) * (size_t)c.cap_p);
+        pr = u + al(std::max<size_t>((size_t)c.cap_a, 2 * (size_t)(c.cap_p + 1)));
+        total = pr + al((size_t)c.cap_p);
+    }
+};
+
+// exclusive scan in place of n (<= 65536) u16 or u32 values in LDS by the whole block: each
+// thread scans a contiguous chunk, chunk sums are block-scanned; a[n] = total. Two barriers in
+// block_excl_scan plus one at the end.
+template <typename V>
+__device__ __forceinline__ uint32_t lds_excl_scan(V* a, uint32_t n, uint32_t* s_wsum) {
+    const uint32_t per = (n + kBlock - 1) / kBlock;
+    const uint32_t c0 = std::min<uint32_t>(threadIdx.x * per, n), c1 = std::min<uint32_t>(c0 + per, n);
+    uint32_t local = 0;
+    for (uint32_t e = c0; e < c1; ++e) local += a[e];
+    uint32_t total;
+    uint32_t run = block_excl_scan(local, s_wsum, &total);
+    for (uint32_t e = c0; e < c1; ++e) {
+        const uint32_t v = a[e];
+        a[e] = (V)run;
+        run += v;
+    }
+    if (threadIdx.x == 0) a[n] = (V)total;
+    __syncthreads();
+    return total;
+}
 
 template <typename T, typename IP, typename OP, typename OI, typename RL>
 __global__ void __launch_bounds__(kBlock)
@@ -333,8 +376,9 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                        unsigned long long capacity, Caps caps, int order, Workspace* ws,
                        unsigned int n_tiles) {
     extern __shared__ __align__(16) unsigned char lds[];
-    __shared__ uint32_t s_rowptr[kBlock + 1];
-    __shared__ uint32_t s_rowc[kBlock];
+    __shared__ uint32_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative)
+    __shared__ uint32_t s_rowS[kBlock + 1];    // row -> first product
+    __shared__ uint32_t s_rowc[kBlock];        // heavy path: row output counts
     __shared__ uint32_t s_wsum[kBlock / 64];
     __shared__ unsigned int s_tile;
     __shared__ int s_heavy;
@@ -357,26 +401,22 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     const int64_t eb = (int64_t)Ap[row0 + nrows];
     const int64_t nnz_t = eb - ea;
 
-    // LDS carve-up of the dynamic region:
-    //   X: eoff[cap_a + 1] (u32)  | later: staged output cols (u16) + vals (T)
-    //   P: pk[cap_p] (u16), pv[cap_p] (T)
-    const size_t x_bytes = std::max<size_t>(sizeof(uint32_t) * (caps.cap_a + 1),
-                                            (sizeof(uint16_t) + sizeof(T)) * caps.cap_p + 16);
-    const size_t x_bytes_al = (x_bytes + 15) & ~size_t(15);
-    uint32_t* s_eoff = reinterpret_cast<uint32_t*>(lds);
-    T* s_ov = reinterpret_cast<T*>(lds);  // staged values (8-aligned start)
-    uint16_t* s_oc = reinterpret_cast<uint16_t*>(lds + sizeof(T) * caps.cap_p);
-    T* s_pv = reinterpret_cast<T*>(lds + x_bytes_al);
-    uint16_t* s_pk = reinterpret_cast<uint16_t*>(lds + x_bytes_al + sizeof(T) * caps.cap_p);
+    const TileLayout L(caps, sizeof(T));
+    uint32_t* s_eoff = reinterpret_cast<uint32_t*>(lds + L.x);
+    T* s_ov = reinterpret_cast<T*>(lds + L.x);
+    uint16_t* s_oc = reinterpret_cast<uint16_t*>(lds + L.x + sizeof(T) * caps.cap_p);
+    T* s_pv = reinterpret_cast<T*>(lds + L.p);
+    uint16_t* s_pk = reinterpret_cast<uint16_t*>(lds + L.p + sizeof(T) * caps.cap_p);
+    uint8_t* s_erow = reinterpret_cast<uint8_t*>(lds + L.u);
+    uint16_t* s_rank = reinterpret_cast<uint16_t*>(lds + L.u);
+    uint8_t* s_prow = reinterpret_cast<uint8_t*>(lds + L.pr);
 
-    bool heavy = nnz_t > caps.cap_a;  // uniform
-    uint32_t d[kMaxE];
-    T x[kMaxE];
-    uint32_t P_t = 0;
-    if (!heavy) {
+    if (nnz_t <= caps.cap_a) {  // uniform
         const uint32_t ne = (uint32_t)nnz_t;
         for (int r = tid; r <= nrows; r += kBlock) s_rowptr[r] = (uint32_t)((int64_t)Ap[row0 + r] - ea);
-        // stage 1a: gather R row descriptors, counts into eoff
+        // ---- stage 1a: coalesced A entries, R descriptor gathers (one word per entry)
+        uint64_t d[kMaxE];
+        T x[kMaxE];
 #pragma unroll
         for (int i = 0; i < kMaxE; ++i) {
             const uint32_t e = tid + i * kBlock;
@@ -392,71 +432,60 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
         }
         __syncthreads();
         STAMP(1);
-        // stage 1b: exclusive scan of counts (contiguous chunk per thread)
-        const uint32_t per = (ne + kBlock - 1) / kBlock;
-        const uint32_t c0 = std::min<uint32_t>(tid * per, ne), c1 = std::min<uint32_t>(c0 + per, ne);
-        uint32_t local = 0;
-        for (uint32_t e = c0; e < c1; ++e) local += s_eoff[e];
-        uint32_t total;
-        uint32_t run = block_excl_scan(local, s_wsum, &total);
-        for (uint32_t e = c0; e < c1; ++e) {
-            const uint32_t c = s_eoff[e];
-            s_eoff[e] = run;
-            run += c;
+        // ---- stage 1b: product offsets per entry; entry -> row map
+        if (tid < nrows)
+            for (uint32_t e = s_rowptr[tid]; e < s_rowptr[tid + 1]; ++e) s_erow[e] = (uint8_t)tid;
+        const uint32_t P_t = lds_excl_scan(s_eoff, ne, s_wsum);
+        for (int r = tid; r <= nrows; r += kBlock) {
+            const uint32_t rs = s_eoff[s_rowptr[r]];
+            s_rowS[r] = rs;
+            if (r < nrows && s_eoff[s_rowptr[r + 1]] - rs > (uint32_t)kRowProdMax) s_heavy = 1;
         }
-        if (tid == 0) s_eoff[ne] = total;
-        P_t = total;
-        __syncthreads();
         STAMP(2);
-        heavy = P_t > (uint32_t)caps.cap_p;  // uniform
-        if (!heavy) {
-            // stage 1c: products into LDS, in (entry, R-entry) order
+        if (P_t <= (uint32_t)caps.cap_p) {  // uniform
+            // ---- stage 1c: every product x*b (one rounding), grouped by row, in (jj, kk) order
 #pragma unroll
             for (int i = 0; i < kMaxE; ++i) {
                 const uint32_t e = tid + i * kBlock;
                 if (e < ne) {
                     const uint32_t o0 = s_eoff[e], o1 = s_eoff[e + 1];
+                    const uint8_t r = s_erow[e];
                     for (uint32_t t = 0; t < o1 - o0; ++t) {
                         uint32_t col;
                         T v;
                         r_product<T>(R, mag, d[i], t, x[i], col, v);
                         s_pk[o0 + t] = (uint16_t)col;
                         s_pv[o0 + t] = v;
+                        s_prow[o0 + t] = r;
                     }
                 }
             }
             __syncthreads();
             STAMP(3);
-            // stage 2: per-row ordered accumulation, list in place at the front of the row's slots
-            uint32_t c = 0, n = 0, s = 0;
-            if (tid < nrows) {
-                s = s_eoff[s_rowptr[tid]];
-                const uint32_t t_end = s_eoff[s_rowptr[tid + 1]];
-                if (t_end - s > (uint32_t)kRowProdMax) {
-                    s_heavy = 1;
-                } else {
-                    for (uint32_t q = s; q < t_end; ++q) {
-                        const uint16_t k = s_pk[q];
-                        const T v = s_pv[q];
-                        uint32_t f = 0;
-                        while (f < n && s_pk[s + f] != k) ++f;
-                        if (f < n) {
-                            s_pv[s + f] = tadd<T>(s_pv[s + f], v);
-                        } else {
-                            s_pk[s + n] = k;
-                            s_pv[s + n] = tadd<T>(T(0), v);
-                            ++n;
-                        }
+            if (!s_heavy) {  // uniform
+                // ---- stage 2: flat over products. A product is the leader of its column group
+                // if no earlier product of its row has that column (= scipy's first touch); the
+                // leader sums the group in sequence order, starting from +0 (sums[k] = 0 first).
+                for (uint32_t q = tid; q < P_t; q += kBlock) {
+                    const uint32_t r = s_prow[q];
+                    const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
+                    const uint16_t k = s_pk[q];
+                    bool leader = true;
+                    for (uint32_t u = rs; u < q; ++u) leader &= s_pk[u] != k;
+                    uint16_t flag = 0;
+                    if (leader) {
+                        T sum = tadd<T>(T(0), s_pv[q]);
+                        for (uint32_t u = q + 1; u < re; ++u)
+                            if (s_pk[u] == k) sum = tadd<T>(sum, s_pv[u]);
+                        s_pv[q] = sum;  // no other leader reads position q (it has column k)
+                        flag = sum != T(0) ? 1 : 0;
                     }
-                    for (uint32_t f = 0; f < n; ++f) c += (s_pv[s + f] != T(0)) ? 1u : 0u;
+                    s_rank[q] = flag;
                 }
-            }
-            __syncthreads();
-            STAMP(4);
-            if (!s_heavy) {
-                // stage 3: tile offsets, look-back, staged coalesced write
-                uint32_t tile_c;
-                const uint32_t o_r = block_excl_scan(tid < nrows ? c : 0u, s_wsum, &tile_c);
+                __syncthreads();
+                STAMP(4);
+                // ---- stage 3: ranks of kept entries (tile-local output positions), look-back
+                const uint32_t tile_c = lds_excl_scan(s_rank, P_t, s_wsum);
                 if (tid < 64) {
                     const unsigned long long g = lookback_wave(states, tile, tile_c, ws);
                     if (tid == 0) s_off = g;
@@ -464,50 +493,31 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 __syncthreads();
                 STAMP(5);
                 const unsigned long long G = s_off;
-                const bool write = G + tile_c <= capacity;
-                if (tid < nrows) {
-                    Cp[row0 + tid] = (OP)(G + o_r);
+                if (tid < nrows) Cp[row0 + tid] = (OP)(G + s_rank[s_rowS[tid]]);
+                for (uint32_t q = tid; q < P_t; q += kBlock) {
+                    const uint32_t rk = s_rank[q];
+                    if (s_rank[q + 1] == rk) continue;  // not a kept leader
+                    const uint32_t r = s_prow[q];
+                    const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
+                    const uint32_t base = s_rank[rs];
+                    uint32_t pos;
                     if (order == RP_ORDER_SORTED) {
-                        // insertion sort of the row's list by column (lists are short)
-                        for (uint32_t a = 1; a < n; ++a) {
-                            const uint16_t kc = s_pk[s + a];
-                            const T kv = s_pv[s + a];
-                            uint32_t b = a;
-                            while (b > 0 && s_pk[s + b - 1] > kc) {
-                                s_pk[s + b] = s_pk[s + b - 1];
-                                s_pv[s + b] = s_pv[s + b - 1];
-                                --b;
-                            }
-                            s_pk[s + b] = kc;
-                            s_pv[s + b] = kv;
-                        }
-                        uint32_t w = o_r;
-                        for (uint32_t f = 0; f < n; ++f) {
-                            const T v = s_pv[s + f];
-                            if (v != T(0)) {
-                                s_oc[w] = s_pk[s + f];
-                                s_ov[w] = v;
-                                ++w;
-                            }
-                        }
+                        const uint16_t k = s_pk[q];
+                        pos = base;
+                        for (uint32_t u = rs; u < re; ++u)
+                            pos += (s_rank[u + 1] != s_rank[u] && s_pk[u] < k) ? 1u : 0u;
                     } else {
-                        uint32_t w = o_r;
-                        for (uint32_t f = n; f-- > 0;) {  // reverse first-touch order
-                            const T v = s_pv[s + f];
-                            if (v != T(0)) {
-                                s_oc[w] = s_pk[s + f];
-                                s_ov[w] = v;
-                                ++w;
-                            }
-                        }
+                        pos = base + (s_rank[re] - 1 - rk);  // reverse first-touch order
                     }
+                    s_oc[pos] = s_pk[q];
+                    s_ov[pos] = s_pv[q];
                 }
                 if (tile == n_tiles - 1 && tid == 0) {
                     Cp[n_rows] = (OP)(G + tile_c);
                     ws->total = G + tile_c;
                 }
                 __syncthreads();
-                if (write) {
+                if (G + tile_c <= capacity) {
                     for (uint32_t q = tid; q < tile_c; q += kBlock) {
                         Cj[G + q] = (OI)s_oc[q];
                         Cx[G + q] = s_ov[q];
@@ -516,7 +526,6 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 STAMP(6);
                 return;
             }
-            heavy = true;
         }
     }
     // ---- exact sequential path (uniform branch)
@@ -687,7 +696,7 @@ struct rp_projector {
     double mag = 0.0;
     int bs = 0;
     // packed
-    DevBuf W, base, O;
+    DevBuf W, O, spare;  // packed image: W (u64 per feature), O (long-row records); spare unused
     // generic
     DevBuf Bp, Bj, Bx32, Bx64;
     // internal workspace and host-path staging
@@ -706,25 +715,26 @@ struct rp_result {
 namespace {
 
 Caps choose_caps(int64_t n_rows, int64_t nnz_a, double prod_per_entry) {
+    // rows per tile: 256 when rows are short (KDD: 11 entries), fewer for long rows or dense R so
+    // a tile's entries fit the register-held stage-1 window (kMaxE per thread) and its products a
+    // ~40 KB LDS tile; caps leave ~6 sigma headroom (a tile beyond them takes the exact slow path)
+    constexpr double kProdBudget = 2816.0;
     Caps c;
-    c.cap_a = kCapAMax;
-    const double avg = n_rows > 0 ? (double)nnz_a / (double)n_rows : 1.0;
-    int rpt = kBlock;
-    const double want = 0.70 * c.cap_a / std::max(avg, 1e-9);
-    if (want < rpt) rpt = std::max(1, (int)want);
-    c.rpt = rpt;
-    const double prods = std::max(1.0, avg * rpt * prod_per_entry);
-    int cp = (int)std::min<double>(c.cap_a, std::max(1024.0, 1.6 * prods + 256.0));
-    c.cap_p = (cp + 63) & ~63;
+    const double avg = n_rows > 0 ? std::max((double)nnz_a / (double)n_rows, 1e-9) : 1.0;
+    const double ppe = std::max(prod_per_entry, 1e-9);
+    const double want = std::min(0.72 * kCapAMax / avg, 0.72 * kProdBudget / (avg * ppe));
+    c.rpt = (int)std::max(1.0, std::min((double)kBlock, want));
+    const double ents = avg * c.rpt;
+    c.cap_a = (int)std::min<double>(kCapAMax, ((int)(1.12 * ents + 6.0 * std::sqrt(ents) + 64.0) + 63) & ~63);
+    const double prods = std::max(1.0, ents * prod_per_entry);
+    c.cap_p = (int)std::min<double>(8192.0, ((int)(1.2 * prods + 8.0 * std::sqrt(prods) + 128.0) + 63) & ~63);
     return c;
 }
 
 size_t lds_bytes_for(const Caps& c, int value_size, int64_t p) {
-    const size_t x = std::max<size_t>(4u * (c.cap_a + 1), (size_t)(2 + value_size) * c.cap_p + 16);
-    const size_t xa = (x + 15) & ~size_t(15);
-    const size_t fast = xa + (size_t)(2 + value_size) * c.cap_p;
+    const TileLayout L(c, (size_t)value_size);
     const size_t heavy = (size_t)(value_size + 2) * (size_t)p;
-    return std::max(fast, heavy);
+    return std::max(L.total, heavy);
 }
 
 template <typename T, typename IP, typename OP, typename OI, typename RL>
@@ -825,7 +835,7 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
         return RP_OK;
     }
     if (h->layout == RP_LAYOUT_PACKED) {
-        PackedR R{(const uint16_t*)h->W.p, (const uint32_t*)h->base.p, (const uint16_t*)h->O.p, h->bs};
+        PackedR R{(const uint64_t*)h->W.p, (const uint16_t*)h->O.p};
         rc = a->data_type == RP_F64
                  ? dispatch_idx<double, PackedR>(R, h->mag, h, a, c, order, ws, n_tiles, caps, lds, st)
                  : dispatch_idx<float, PackedR>(R, (float)h->mag, h, a, c, order, ws, n_tiles, caps, lds, st);
@@ -856,8 +866,7 @@ struct HostImage {
     double mag = 0.0;
     int bs = 0;
     int64_t nnz = 0, b0 = 0;
-    std::vector<uint16_t> W;
-    std::vector<uint32_t> base;
+    std::vector<uint64_t> W;
     std::vector<uint16_t> O;
     std::vector<int32_t> Bp;
     std::vector<uint16_t> Bj;
@@ -884,7 +893,7 @@ int build_image(int64_t m, int64_t p, const void* indptr, int32_t indptr_type, c
             return fail(RP_ERR_INVALID, "R indptr not monotone");
     // validate columns and detect the single-magnitude layout
     double mag = 0.0;
-    bool single = p <= 8192 && nnz > 0;
+    bool single = p <= 16384 && nnz > 0;
     for (int64_t q = 0; q < nnz; ++q) {
         const int64_t col = ptr_at(indices, indices_type, b0 + q);
         if (col < 0 || col >= p) return fail(RP_ERR_INVALID, "R column index %lld out of range", (long long)col);
@@ -909,62 +918,40 @@ int build_image(int64_t m, int64_t p, const void* indptr, int32_t indptr_type, c
     }
     img.layout = RP_LAYOUT_PACKED;
     img.mag = mag;
-    // block shift: every block's overflow region must be addressable with 15 bits
-    int bs = 12;
-    std::vector<uint64_t> need;
-    for (;; --bs) {
-        const int64_t nb = (m + ((int64_t)1 << bs) - 1) >> bs;
-        need.assign((size_t)std::max<int64_t>(nb, 1), 0);
-        for (int64_t j = 0; j < m; ++j) {
-            const int64_t cnt = ptr_at(indptr, indptr_type, j + 1) - ptr_at(indptr, indptr_type, j);
-            if (cnt >= 2) need[(size_t)(j >> bs)] += 1 + (uint64_t)cnt;
-        }
-        bool ok = true;
-        for (uint64_t v : need) ok &= v <= 32767;
-        if (ok || bs == 0) break;
-    }
-    img.bs = bs;
-    const int64_t nb = (int64_t)need.size();
-    img.base.resize((size_t)nb);
-    uint64_t acc = 0;
-    for (int64_t b = 0; b < nb; ++b) {
-        img.base[(size_t)b] = (uint32_t)acc;
-        acc += need[(size_t)b];
-    }
-    if (acc >= ((uint64_t)1 << 31)) return fail(RP_ERR_UNSUPPORTED, "overflow table too large");
+    img.bs = 0;
     img.W.assign((size_t)m, 0);
-    img.O.assign((size_t)acc, 0);
-    std::vector<uint64_t> fill(img.base.begin(), img.base.end());
+    img.O.clear();
     for (int64_t j = 0; j < m; ++j) {
         const int64_t s0 = ptr_at(indptr, indptr_type, j), t0 = ptr_at(indptr, indptr_type, j + 1);
         const int64_t cnt = t0 - s0;
-        if (cnt == 1) {
-            const uint32_t col = (uint32_t)ptr_at(indices, indices_type, s0);
-            const bool neg = val_at(data, data_type, s0) < 0;
-            img.W[(size_t)j] = (uint16_t)(0x4000u | (neg ? 0x2000u : 0u) | col);
-        } else if (cnt >= 2) {
-            const size_t b = (size_t)(j >> bs);
-            const uint64_t rec = fill[b];
-            img.W[(size_t)j] = (uint16_t)(0x8000u | (uint32_t)(rec - img.base[b]));
-            img.O[rec] = (uint16_t)cnt;
+        if (cnt <= 4) {
+            uint64_t w = (uint64_t)cnt << 61;
+            for (int64_t q = 0; q < cnt; ++q) {
+                const uint64_t col = (uint64_t)ptr_at(indices, indices_type, s0 + q);
+                const bool neg = val_at(data, data_type, s0 + q) < 0;
+                w |= ((neg ? 0x4000ull : 0ull) | col) << (15 * q);
+            }
+            img.W[(size_t)j] = w;
+        } else {
+            img.W[(size_t)j] = kOvf | (uint64_t)img.O.size();
+            img.O.push_back((uint16_t)cnt);
             for (int64_t q = 0; q < cnt; ++q) {
                 const uint32_t col = (uint32_t)ptr_at(indices, indices_type, s0 + q);
                 const bool neg = val_at(data, data_type, s0 + q) < 0;
-                img.O[rec + 1 + (uint64_t)q] = (uint16_t)((neg ? 0x8000u : 0u) | col);
+                img.O.push_back((uint16_t)((neg ? 0x8000u : 0u) | col));
             }
-            fill[b] += 1 + (uint64_t)cnt;
         }
     }
     return RP_OK;
 }
 
-// the three buffers of an image: packed W/base/O, or generic Bp/Bj/values (values from the caller)
+// the three buffers of an image: packed W/O/-, or generic Bp/Bj/values (values from the caller)
 void image_parts(const HostImage& img, const void* data, int32_t data_type, const void* src[3],
                  int64_t bytes[3]) {
     if (img.layout == RP_LAYOUT_PACKED) {
-        src[0] = img.W.data(); bytes[0] = 2 * (int64_t)img.W.size();
-        src[1] = img.base.data(); bytes[1] = 4 * (int64_t)img.base.size();
-        src[2] = img.O.data(); bytes[2] = 2 * (int64_t)img.O.size();
+        src[0] = img.W.data(); bytes[0] = 8 * (int64_t)img.W.size();
+        src[1] = img.O.data(); bytes[1] = 2 * (int64_t)img.O.size();
+        src[2] = nullptr; bytes[2] = 0;
     } else {
         const int vs = dtype_size(data_type);
         src[0] = img.Bp.data(); bytes[0] = 4 * (int64_t)img.Bp.size();
@@ -1030,7 +1017,7 @@ int rp_projector_create(int device, int64_t m, int64_t p, const void* indptr, in
     image_parts(img, data, data_type, src, bytes);
     DevBuf* dst[3];
     if (img.layout == RP_LAYOUT_PACKED) {
-        dst[0] = &h->W; dst[1] = &h->base; dst[2] = &h->O;
+        dst[0] = &h->W; dst[1] = &h->O; dst[2] = &h->spare;
     } else {
         dst[0] = &h->Bp; dst[1] = &h->Bj; dst[2] = data_type == RP_F64 ? &h->Bx64 : &h->Bx32;
     }
@@ -1090,8 +1077,8 @@ int rp_projector_info_get(const rp_projector* h, rp_projector_info* out) {
     if (h->layout == RP_LAYOUT_PACKED) {
         out->n_buffers = 3;
         out->buffer_bytes[0] = (int64_t)h->W.bytes;
-        out->buffer_bytes[1] = (int64_t)h->base.bytes;
-        out->buffer_bytes[2] = (int64_t)h->O.bytes;
+        out->buffer_bytes[1] = (int64_t)h->O.bytes;
+        out->buffer_bytes[2] = 0;
     } else {
         out->n_buffers = 3;
         out->buffer_bytes[0] = (int64_t)h->Bp.bytes;
@@ -1104,7 +1091,7 @@ int rp_projector_info_get(const rp_projector* h, rp_projector_info* out) {
 
 static const DevBuf* image_buffer(const rp_projector* h, int which) {
     if (h->layout == RP_LAYOUT_PACKED) {
-        const DevBuf* b[3] = {&h->W, &h->base, &h->O};
+        const DevBuf* b[3] = {&h->W, &h->O, &h->spare};
         return (which >= 0 && which < 3) ? b[which] : nullptr;
     }
     const DevBuf* b[3] = {&h->Bp, &h->Bj, h->value_type == RP_F64 ? &h->Bx64 : &h->Bx32};
@@ -1145,7 +1132,7 @@ int rp_projector_create_from_device(int device, const rp_projector_info* info,
     }
     DevBuf* dst[3];
     if (h->layout == RP_LAYOUT_PACKED) {
-        dst[0] = &h->W; dst[1] = &h->base; dst[2] = &h->O;
+        dst[0] = &h->W; dst[1] = &h->O; dst[2] = &h->spare;
     } else {
         dst[0] = &h->Bp; dst[1] = &h->Bj; dst[2] = h->value_type == RP_F64 ? &h->Bx64 : &h->Bx32;
     }

@@ -23,23 +23,26 @@ def pack(R, layout=nat.RP_LAYOUT_AUTO):
 
 
 def decode_packed(info, bufs, dtype):
-    W = bufs[0][:info.buffer_bytes[0]].view(np.uint16)
-    base = bufs[1][:info.buffer_bytes[1]].view(np.uint32)
-    O = bufs[2][:info.buffer_bytes[2]].view(np.uint16)
+    """Decode the 64-bit packed image: n = w >> 61 entries inline (15 bits each:
+    sign << 14 | column), or n == 7: record at O[w & (2^61-1)] = count, (sign << 15 | column)..."""
+    W = bufs[0][:info.buffer_bytes[0]].view(np.uint64)
+    O = bufs[1][:info.buffer_bytes[1]].view(np.uint16)
     mag = dtype(info.magnitude)
     indptr, cols, vals = [0], [], []
-    for j, w in enumerate(W.tolist()):
-        if w & 0x8000:
-            rec = int(base[j >> info.block_shift]) + (w & 0x7FFF)
-            n = int(O[rec])
-            ent = O[rec + 1: rec + 1 + n].astype(np.int64)
+    for w in W.tolist():
+        n = w >> 61
+        if n == 7:
+            rec = w & ((1 << 61) - 1)
+            k = int(O[rec])
+            ent = O[rec + 1: rec + 1 + k].astype(np.int64)
             cols.extend((ent & 0x7FFF).tolist())
             vals.extend(np.where(ent & 0x8000, -mag, mag).tolist())
-        elif w & 0x4000:
-            cols.append(w & 0x1FFF)
-            vals.append(-mag if w & 0x2000 else mag)
         else:
-            assert w == 0
+            assert w >> (15 * n) & ((1 << (61 - 15 * n)) - 1) == 0   # unused bits are clear
+            for t in range(n):
+                e = (w >> (15 * t)) & 0x7FFF
+                cols.append(e & 0x3FFF)
+                vals.append(-mag if e & 0x4000 else mag)
         indptr.append(len(cols))
     return np.array(indptr), np.array(cols), np.array(vals, dtype=dtype)
 
@@ -53,22 +56,22 @@ def test_packed_roundtrip(m, p, dtype):
     ip, ix, vx = decode_packed(info, bufs, dtype)
     assert np.array_equal(ip, R.indptr) and np.array_equal(ix, R.indices)
     assert np.array_equal(vx.view(np.uint8), R.data.view(np.uint8))
-    assert info.buffer_bytes[0] == 2 * m                       # one u16 word per feature
+    assert info.buffer_bytes[0] == 8 * m                       # one u64 word per feature
 
 
-def test_block_shift_shrinks_for_dense_rows():
-    """Features with many entries overflow a 4096-feature block's 15-bit record offsets: the
-    packer picks a smaller block."""
+def test_long_rows_use_records():
+    """Features with more than 4 entries are stored as records; order and signs survive."""
     rng = np.random.default_rng(0)
-    m, p = 8192, 4096
-    rows = [np.sort(rng.choice(p, size=40, replace=False)) for _ in range(m)]
-    indptr = np.arange(m + 1) * 40
-    R = sp.csr_matrix((np.where(rng.random(m * 40) < .5, -1.0, 1.0).astype(np.float32), np.concatenate(rows), indptr),
-                      shape=(m, p))
+    m, p = 3000, 16384
+    k = rng.integers(0, 12, size=m)
+    rows = [rng.choice(p, size=int(x), replace=False) for x in k]     # unsorted storage order
+    indptr = np.concatenate([[0], np.cumsum(k)])
+    R = sp.csr_matrix((np.where(rng.random(indptr[-1]) < .5, -2.5, 2.5).astype(np.float32),
+                       np.concatenate(rows), indptr), shape=(m, p))
     info, bufs = pack(R)
-    assert info.layout == nat.RP_LAYOUT_PACKED and info.block_shift < 12
+    assert info.layout == nat.RP_LAYOUT_PACKED and info.buffer_bytes[1] > 0
     ip, ix, vx = decode_packed(info, bufs, np.float32)
-    assert np.array_equal(ix, R.indices) and np.array_equal(vx, R.data)
+    assert np.array_equal(ip, R.indptr) and np.array_equal(ix, R.indices) and np.array_equal(vx, R.data)
 
 
 def test_generic_when_magnitudes_differ_or_forced():
