@@ -329,27 +329,25 @@ struct Caps {
     int rpt;     // rows per tile (<= kBlock)
 };
 
-// Dynamic-LDS carve-up of a tile (host sizes it, device uses it; all offsets 16-byte aligned):
-//   X  : eoff[cap_a + 1] (u32, stage 1)            | staged output cols (u16) + vals (T) (stage 3)
-//   P  : pv[cap_p] (T), pk[cap_p] (u16)             products, then leaders' sums in place
-//   U  : erow[cap_a] (u8, stage 1)                  | flag/rank[cap_p + 1] (u16, stages 2-3)
-//   PR : prow[cap_p] (u8)                           row of each product
+// Dynamic-LDS carve-up of a tile (host sizes it, device uses it; offsets 16-byte aligned):
+//   X : eoff[cap_a + 1] (u16)                      product offset of every A entry (stage 1)
+//   U : erow[cap_a] (u8, stage 1) | rank[cap_p + 1] (u16, stages 2-3)
+//   P : pv[cap_p] (T), pkr[cap_p] (u32 = row << 16 | column)   products; leaders' sums in place
+// The exact slow path reuses the whole region as scipy's dense sums[p]/next[p] accumulator.
 struct TileLayout {
-    size_t x, p, u, pr, total;
+    size_t x, u, pv, pkr, total;
     __host__ __device__ TileLayout(const Caps& c, size_t vs) {
         auto al = [](size_t v) { return (v + 15) & ~size_t(15); };
-        const size_t xb = std::max<size_t>(4 * (size_t)(c.cap_a + 1), (2 + vs) * (size_t)c.cap_p + 16);
         x = 0;
-        p = al(xb);
-        u = p + al((2 + vs) * (size_t)c.cap_p);
-        pr = u + al(std::max<size_t>((size_t)c.cap_a, 2 * (size_t)(c.cap_p + 1)));
-        total = pr + al((size_t)c.cap_p);
+        u = al(2 * (size_t)(c.cap_a + 1));
+        pv = u + al(std::max<size_t>((size_t)c.cap_a, 2 * (size_t)(c.cap_p + 1)));
+        pkr = pv + al(vs * (size_t)c.cap_p);
+        total = pkr + al(4 * (size_t)c.cap_p);
     }
 };
 
-// exclusive scan in place of n (<= 65536) u16 or u32 values in LDS by the whole block: each
-// thread scans a contiguous chunk, chunk sums are block-scanned; a[n] = total. Two barriers in
-// block_excl_scan plus one at the end.
+// exclusive scan in place of n (<= 65535 total) u16 or u32 values in LDS by the whole block:
+// each thread scans a contiguous chunk, chunk sums are block-scanned; a[n] = total (u32 return).
 template <typename V>
 __device__ __forceinline__ uint32_t lds_excl_scan(V* a, uint32_t n, uint32_t* s_wsum) {
     const uint32_t per = (n + kBlock - 1) / kBlock;
@@ -376,9 +374,8 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                        unsigned long long capacity, Caps caps, int order, Workspace* ws,
                        unsigned int n_tiles) {
     extern __shared__ __align__(16) unsigned char lds[];
-    __shared__ uint32_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative)
-    __shared__ uint32_t s_rowS[kBlock + 1];    // row -> first product
-    __shared__ uint32_t s_rowc[kBlock];        // heavy path: row output counts
+    __shared__ uint16_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative, <= cap_a)
+    __shared__ uint16_t s_rowS[kBlock + 1];    // row -> first product
     __shared__ uint32_t s_wsum[kBlock / 64];
     __shared__ unsigned int s_tile;
     __shared__ int s_heavy;
@@ -402,19 +399,16 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     const int64_t nnz_t = eb - ea;
 
     const TileLayout L(caps, sizeof(T));
-    uint32_t* s_eoff = reinterpret_cast<uint32_t*>(lds + L.x);
-    T* s_ov = reinterpret_cast<T*>(lds + L.x);
-    uint16_t* s_oc = reinterpret_cast<uint16_t*>(lds + L.x + sizeof(T) * caps.cap_p);
-    T* s_pv = reinterpret_cast<T*>(lds + L.p);
-    uint16_t* s_pk = reinterpret_cast<uint16_t*>(lds + L.p + sizeof(T) * caps.cap_p);
+    uint16_t* s_eoff = reinterpret_cast<uint16_t*>(lds + L.x);
     uint8_t* s_erow = reinterpret_cast<uint8_t*>(lds + L.u);
     uint16_t* s_rank = reinterpret_cast<uint16_t*>(lds + L.u);
-    uint8_t* s_prow = reinterpret_cast<uint8_t*>(lds + L.pr);
+    T* s_pv = reinterpret_cast<T*>(lds + L.pv);
+    uint32_t* s_pkr = reinterpret_cast<uint32_t*>(lds + L.pkr);
 
     if (nnz_t <= caps.cap_a) {  // uniform
         const uint32_t ne = (uint32_t)nnz_t;
-        for (int r = tid; r <= nrows; r += kBlock) s_rowptr[r] = (uint32_t)((int64_t)Ap[row0 + r] - ea);
-        // ---- stage 1a: coalesced A entries, R descriptor gathers (one word per entry)
+        for (int r = tid; r <= nrows; r += kBlock) s_rowptr[r] = (uint16_t)((int64_t)Ap[row0 + r] - ea);
+        // ---- stage 1a: coalesced A entries, one R-descriptor gather per entry
         uint64_t d[kMaxE];
         T x[kMaxE];
 #pragma unroll
@@ -427,64 +421,65 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 x[i] = Ax[ea + e];
                 uint32_t cnt;
                 d[i] = r_describe<T>(R, j, cnt);
-                s_eoff[e] = cnt;
+                s_eoff[e] = (uint16_t)std::min<uint32_t>(cnt, 0xffffu);
             }
         }
         __syncthreads();
         STAMP(1);
-        // ---- stage 1b: product offsets per entry; entry -> row map
+        // ---- stage 1b: product offsets per entry; entry -> row map; row product ranges
         if (tid < nrows)
             for (uint32_t e = s_rowptr[tid]; e < s_rowptr[tid + 1]; ++e) s_erow[e] = (uint8_t)tid;
         const uint32_t P_t = lds_excl_scan(s_eoff, ne, s_wsum);
-        for (int r = tid; r <= nrows; r += kBlock) {
-            const uint32_t rs = s_eoff[s_rowptr[r]];
-            s_rowS[r] = rs;
-            if (r < nrows && s_eoff[s_rowptr[r + 1]] - rs > (uint32_t)kRowProdMax) s_heavy = 1;
-        }
+        const bool fits = P_t <= (uint32_t)caps.cap_p;  // uniform; if not, offsets wrapped: slow path
+        if (fits)
+            for (int r = tid; r <= nrows; r += kBlock) {
+                const uint32_t rs = s_eoff[s_rowptr[r]];
+                s_rowS[r] = (uint16_t)rs;
+                if (r < nrows && s_eoff[s_rowptr[r + 1]] - rs > (uint32_t)kRowProdMax) s_heavy = 1;
+            }
         STAMP(2);
-        if (P_t <= (uint32_t)caps.cap_p) {  // uniform
+        if (fits) {
             // ---- stage 1c: every product x*b (one rounding), grouped by row, in (jj, kk) order
 #pragma unroll
             for (int i = 0; i < kMaxE; ++i) {
                 const uint32_t e = tid + i * kBlock;
                 if (e < ne) {
                     const uint32_t o0 = s_eoff[e], o1 = s_eoff[e + 1];
-                    const uint8_t r = s_erow[e];
+                    const uint32_t rtag = (uint32_t)s_erow[e] << 16;
                     for (uint32_t t = 0; t < o1 - o0; ++t) {
                         uint32_t col;
                         T v;
                         r_product<T>(R, mag, d[i], t, x[i], col, v);
-                        s_pk[o0 + t] = (uint16_t)col;
+                        s_pkr[o0 + t] = rtag | col;
                         s_pv[o0 + t] = v;
-                        s_prow[o0 + t] = r;
                     }
                 }
             }
             __syncthreads();
             STAMP(3);
             if (!s_heavy) {  // uniform
-                // ---- stage 2: flat over products. A product is the leader of its column group
-                // if no earlier product of its row has that column (= scipy's first touch); the
-                // leader sums the group in sequence order, starting from +0 (sums[k] = 0 first).
+                // ---- stage 2: flat over products. A product leads its column group if no earlier
+                // product of its row has that column (= scipy's first touch); the leader sums the
+                // group in sequence order starting from +0 (scipy: sums[k] = 0, then +=).
                 for (uint32_t q = tid; q < P_t; q += kBlock) {
-                    const uint32_t r = s_prow[q];
+                    const uint32_t kr = s_pkr[q];
+                    const uint32_t r = kr >> 16;
                     const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
-                    const uint16_t k = s_pk[q];
                     bool leader = true;
-                    for (uint32_t u = rs; u < q; ++u) leader &= s_pk[u] != k;
+                    for (uint32_t u = rs; u < q; ++u) leader &= s_pkr[u] != kr;
                     uint16_t flag = 0;
                     if (leader) {
                         T sum = tadd<T>(T(0), s_pv[q]);
                         for (uint32_t u = q + 1; u < re; ++u)
-                            if (s_pk[u] == k) sum = tadd<T>(sum, s_pv[u]);
-                        s_pv[q] = sum;  // no other leader reads position q (it has column k)
+                            if (s_pkr[u] == kr) sum = tadd<T>(sum, s_pv[u]);
+                        s_pv[q] = sum;  // position q is read by no other leader (column differs)
                         flag = sum != T(0) ? 1 : 0;
                     }
                     s_rank[q] = flag;
                 }
                 __syncthreads();
                 STAMP(4);
-                // ---- stage 3: ranks of kept entries (tile-local output positions), look-back
+                // ---- stage 3: ranks of kept entries = tile-local output positions; look-back
                 const uint32_t tile_c = lds_excl_scan(s_rank, P_t, s_wsum);
                 if (tid < 64) {
                     const unsigned long long g = lookback_wave(states, tile, tile_c, ws);
@@ -494,42 +489,38 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 STAMP(5);
                 const unsigned long long G = s_off;
                 if (tid < nrows) Cp[row0 + tid] = (OP)(G + s_rank[s_rowS[tid]]);
-                for (uint32_t q = tid; q < P_t; q += kBlock) {
-                    const uint32_t rk = s_rank[q];
-                    if (s_rank[q + 1] == rk) continue;  // not a kept leader
-                    const uint32_t r = s_prow[q];
-                    const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
-                    const uint32_t base = s_rank[rs];
-                    uint32_t pos;
-                    if (order == RP_ORDER_SORTED) {
-                        const uint16_t k = s_pk[q];
-                        pos = base;
-                        for (uint32_t u = rs; u < re; ++u)
-                            pos += (s_rank[u + 1] != s_rank[u] && s_pk[u] < k) ? 1u : 0u;
-                    } else {
-                        pos = base + (s_rank[re] - 1 - rk);  // reverse first-touch order
+                if (G + tile_c <= capacity) {
+                    // kept leaders write straight into the tile's contiguous output range
+                    for (uint32_t q = tid; q < P_t; q += kBlock) {
+                        const uint32_t rk = s_rank[q];
+                        if (s_rank[q + 1] == rk) continue;  // not a kept leader
+                        const uint32_t kr = s_pkr[q];
+                        const uint32_t r = kr >> 16;
+                        const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
+                        uint32_t pos = s_rank[rs];
+                        if (order == RP_ORDER_SORTED) {
+                            for (uint32_t u = rs; u < re; ++u)
+                                pos += (s_rank[u + 1] != s_rank[u] && s_pkr[u] < kr) ? 1u : 0u;
+                        } else {
+                            pos += s_rank[re] - 1 - rk;  // reverse first-touch order
+                        }
+                        Cj[G + pos] = (OI)(kr & 0xffffu);
+                        Cx[G + pos] = s_pv[q];
                     }
-                    s_oc[pos] = s_pk[q];
-                    s_ov[pos] = s_pv[q];
                 }
                 if (tile == n_tiles - 1 && tid == 0) {
                     Cp[n_rows] = (OP)(G + tile_c);
                     ws->total = G + tile_c;
                 }
-                __syncthreads();
-                if (G + tile_c <= capacity) {
-                    for (uint32_t q = tid; q < tile_c; q += kBlock) {
-                        Cj[G + q] = (OI)s_oc[q];
-                        Cx[G + q] = s_ov[q];
-                    }
-                }
                 STAMP(6);
                 return;
             }
         }
+        __syncthreads();
     }
-    // ---- exact sequential path (uniform branch)
+    // ---- exact sequential path (uniform branch); row counts kept in the rank region's tail
     STAMP(7);
+    uint32_t* s_rowc = reinterpret_cast<uint32_t*>(lds + L.total - 4 * kBlock);
     heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, 0, 0, Cp, Cj,
                                   Cx, false, order);
     uint32_t tile_c;
@@ -725,15 +716,17 @@ Caps choose_caps(int64_t n_rows, int64_t nnz_a, double prod_per_entry) {
     const double want = std::min(0.72 * kCapAMax / avg, 0.72 * kProdBudget / (avg * ppe));
     c.rpt = (int)std::max(1.0, std::min((double)kBlock, want));
     const double ents = avg * c.rpt;
-    c.cap_a = (int)std::min<double>(kCapAMax, ((int)(1.12 * ents + 6.0 * std::sqrt(ents) + 64.0) + 63) & ~63);
+    // 6 sigma of a sum of rpt Poisson-like row lengths (sd ~ sqrt(ents)); the products' sd is
+    // ~1.25 sqrt(products) for single-magnitude SRP matrices (compound of R-row counts)
+    c.cap_a = (int)std::min<double>(kCapAMax, ((int)(ents + 6.0 * std::sqrt(ents) + 40.0) + 63) & ~63);
     const double prods = std::max(1.0, ents * prod_per_entry);
-    c.cap_p = (int)std::min<double>(8192.0, ((int)(1.2 * prods + 8.0 * std::sqrt(prods) + 128.0) + 63) & ~63);
+    c.cap_p = (int)std::min<double>(8192.0, ((int)(prods + 7.5 * std::sqrt(prods) + 40.0) + 63) & ~63);
     return c;
 }
 
 size_t lds_bytes_for(const Caps& c, int value_size, int64_t p) {
     const TileLayout L(c, (size_t)value_size);
-    const size_t heavy = (size_t)(value_size + 2) * (size_t)p;
+    const size_t heavy = (((size_t)(value_size + 2) * (size_t)p + 15) & ~size_t(15)) + 4 * kBlock;
     return std::max(L.total, heavy);
 }
 
