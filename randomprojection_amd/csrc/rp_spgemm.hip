@@ -239,55 +239,103 @@ __device__ unsigned long long lookback_wave(unsigned long long* states, unsigned
 }
 
 // ------------------------------------------------------------------------------------------
-// exact sequential path for tiles beyond the LDS caps: scipy's dense sums/next accumulator in
-// LDS, one lane. Pass 0 counts, pass 1 writes (after the look-back gave the tile offset).
+// Exact slow path for tiles beyond the LDS caps: scipy's dense sums[p]/next[p] accumulator in LDS.
+// Rows are done one after another; a row's entries stream in chunks of 256 (parallel gathers,
+// products staged in LDS in (jj, kk) order), and one lane accumulates them in order. Pass 0 counts
+// (row counts -> s_rowc), pass 1 writes at the tile offset from the look-back.
+constexpr int kHeavyBuf = 32;   // staged products per chunk
+
+__host__ __device__ inline size_t heavy_lds_bytes(int64_t p, size_t vs) {
+    const size_t acc = (((size_t)p * (vs + 2)) + 15) & ~size_t(15);
+    return acc + ((2 * kHeavyBuf + 15) & ~size_t(15)) + vs * kHeavyBuf + 4 * kBlock;  // + row counts
+}
+
 template <typename T, typename IP, typename OP, typename OI, typename RL>
 __device__ void heavy_tile(const RL& R, T mag, const IP* __restrict__ Ap,
                            const int32_t* __restrict__ Aj, const T* __restrict__ Ax, int64_t row0,
-                           int nrows, int p, unsigned char* lds, uint32_t* s_rowc, int pass,
-                           unsigned long long tile_off, OP* __restrict__ Cp,
-                           OI* __restrict__ Cj, T* __restrict__ Cx, bool write_entries,
-                           int order) {
+                           int nrows, int p, unsigned char* lds, uint32_t* s_rowc, uint32_t* s_wsum,
+                           int pass, unsigned long long tile_off, OP* __restrict__ Cp,
+                           OI* __restrict__ Cj, T* __restrict__ Cx, bool write_entries, int order) {
+    __shared__ int s_take, s_end;
+    const size_t vs = sizeof(T);
     T* sums = reinterpret_cast<T*>(lds);
-    int16_t* next = reinterpret_cast<int16_t*>(lds + sizeof(T) * (size_t)p);
-    for (int k = threadIdx.x; k < p; k += kBlock) {
+    int16_t* next = reinterpret_cast<int16_t*>(lds + vs * (size_t)p);
+    unsigned char* buf = lds + ((((size_t)p * (vs + 2)) + 15) & ~size_t(15));
+    uint16_t* s_hk = reinterpret_cast<uint16_t*>(buf);
+    T* s_hv = reinterpret_cast<T*>(buf + ((2 * kHeavyBuf + 15) & ~size_t(15)));
+    const int tid = threadIdx.x;
+    for (int k = tid; k < p; k += kBlock) {
         sums[k] = T(0);
         next[k] = -1;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long off = tile_off;
-        for (int r = 0; r < nrows; ++r) {
-            int head = -2, length = 0;
-            const int64_t jb = (int64_t)Ap[row0 + r], je = (int64_t)Ap[row0 + r + 1];
-            for (int64_t jj = jb; jj < je; ++jj) {
-                const int32_t j = Aj[jj];
-                const T x = Ax[jj];
-                uint32_t cnt;
-                const uint64_t d = r_describe<T>(R, j, cnt);
-                for (uint32_t t = 0; t < cnt; ++t) {
-                    uint32_t k;
-                    T v;
-                    r_product<T>(R, mag, d, t, x, k, v);
-                    sums[k] = tadd<T>(sums[k], v);
-                    if (next[k] == -1) {
-                        next[k] = (int16_t)head;
-                        head = (int)k;
-                        ++length;
-                    }
-                }
+    unsigned long long off = tile_off;
+    int head = -2, length = 0;  // meaningful on lane 0 only
+    auto touch = [&](uint32_t k, T v) {
+        sums[k] = tadd<T>(sums[k], v);
+        if (next[k] == -1) {
+            next[k] = (int16_t)head;
+            head = (int)k;
+            ++length;
+        }
+    };
+    for (int r = 0; r < nrows; ++r) {
+        const int64_t jb = (int64_t)Ap[row0 + r], je = (int64_t)Ap[row0 + r + 1];
+        head = -2;
+        length = 0;
+        for (int64_t c = jb; c < je;) {
+            const int64_t e = c + tid;
+            uint32_t cnt = 0;
+            uint64_t d = 0;
+            T x = T(0);
+            if (e < je) {
+                x = Ax[e];
+                d = r_describe<T>(R, Aj[e], cnt);
             }
-            uint32_t c = 0;
+            uint32_t tot;
+            const uint32_t excl = block_excl_scan(cnt, s_wsum, &tot);
+            const bool fits = e < je && excl + cnt <= (uint32_t)kHeavyBuf;
+            const int take = __syncthreads_count(fits);
+            if (take > 0) {
+                if (fits) {
+                    for (uint32_t t = 0; t < cnt; ++t) {
+                        uint32_t col;
+                        T v;
+                        r_product<T>(R, mag, d, t, x, col, v);
+                        s_hk[excl + t] = (uint16_t)col;
+                        s_hv[excl + t] = v;
+                    }
+                    if (tid == take - 1) s_end = (int)(excl + cnt);
+                }
+                __syncthreads();
+                if (tid == 0)
+                    for (int q = 0; q < s_end; ++q) touch(s_hk[q], s_hv[q]);
+                if (tid == 0) s_take = take;
+            } else if (tid == 0) {  // one entry with more than kHeavyBuf products: straight from R
+                for (uint32_t t = 0; t < cnt; ++t) {
+                    uint32_t col;
+                    T v;
+                    r_product<T>(R, mag, d, t, x, col, v);
+                    touch(col, v);
+                }
+                s_take = 1;
+            }
+            __syncthreads();
+            c += s_take;
+            __syncthreads();
+        }
+        if (tid == 0) {
+            uint32_t cnt_r = 0;
             const unsigned long long row_off = off;
             for (int q = 0; q < length; ++q) {
-                const T s = sums[head];
-                if (s != T(0)) {
+                const T sv = sums[head];
+                if (sv != T(0)) {
                     if (pass == 1 && write_entries) {
                         Cj[off] = (OI)head;
-                        Cx[off] = s;
+                        Cx[off] = sv;
                     }
                     ++off;
-                    ++c;
+                    ++cnt_r;
                 }
                 const int tmp = head;
                 head = next[head];
@@ -295,12 +343,11 @@ __device__ void heavy_tile(const RL& R, T mag, const IP* __restrict__ Ap,
                 sums[tmp] = T(0);
             }
             if (pass == 0) {
-                s_rowc[r] = c;
+                s_rowc[r] = cnt_r;
             } else {
                 Cp[row0 + r] = (OP)row_off;
-                if (order == RP_ORDER_SORTED && write_entries && c > 1) {
-                    // shell sort of the row segment by column (rare path)
-                    const unsigned long long n = c;
+                if (order == RP_ORDER_SORTED && write_entries && cnt_r > 1) {
+                    const unsigned long long n = cnt_r;  // shell sort of the row segment (rare path)
                     for (unsigned long long gap = n / 2; gap > 0; gap /= 2)
                         for (unsigned long long a = gap; a < n; ++a) {
                             OI kc = Cj[row_off + a];
@@ -317,8 +364,8 @@ __device__ void heavy_tile(const RL& R, T mag, const IP* __restrict__ Ap,
                 }
             }
         }
+        __syncthreads();
     }
-    __syncthreads();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -518,11 +565,11 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
         }
         __syncthreads();
     }
-    // ---- exact sequential path (uniform branch); row counts kept in the rank region's tail
+    // ---- exact slow path (uniform branch)
     STAMP(7);
-    uint32_t* s_rowc = reinterpret_cast<uint32_t*>(lds + L.total - 4 * kBlock);
-    heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, 0, 0, Cp, Cj,
-                                  Cx, false, order);
+    uint32_t* s_rowc = reinterpret_cast<uint32_t*>(lds + heavy_lds_bytes(p, sizeof(T)) - 4 * kBlock);
+    heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 0, 0,
+                                  Cp, Cj, Cx, false, order);
     uint32_t tile_c;
     (void)block_excl_scan(tid < nrows ? s_rowc[tid] : 0u, s_wsum, &tile_c);
     if (tid < 64) {
@@ -532,8 +579,8 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     __syncthreads();
     const unsigned long long G = s_off;
     const bool write = G + tile_c <= capacity;
-    heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, 1, G, Cp, Cj,
-                                  Cx, write, order);
+    heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 1, G,
+                                  Cp, Cj, Cx, write, order);
     if (tile == n_tiles - 1 && tid == 0) {
         Cp[n_rows] = (OP)(G + tile_c);
         ws->total = G + tile_c;
@@ -726,8 +773,7 @@ Caps choose_caps(int64_t n_rows, int64_t nnz_a, double prod_per_entry) {
 
 size_t lds_bytes_for(const Caps& c, int value_size, int64_t p) {
     const TileLayout L(c, (size_t)value_size);
-    const size_t heavy = (((size_t)(value_size + 2) * (size_t)p + 15) & ~size_t(15)) + 4 * kBlock;
-    return std::max(L.total, heavy);
+    return std::max(L.total, heavy_lds_bytes(p, (size_t)value_size));
 }
 
 template <typename T, typename IP, typename OP, typename OI, typename RL>
