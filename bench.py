@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+RANDOM_LINE_CEILING = 55e9  # random 128-B line fills/s, measured (scripts/probes/gather_probe*.hip)
 
 
 def log(*a):
@@ -175,6 +176,10 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:  # noqa: BLE001
             traffic = None
+    # the ceiling that binds this kernel: one random R-descriptor gather per A entry, each a full
+    # 128-B line fill; measured on MI355X at ~55 G random lines/s for any table from 32 MB to 2 GB,
+    # any load flavour or allocation (profiles/r01_probe_gather_*.json)
+    gathers_per_s = nnz_a / (kernel_ms * 1e-3)
 
     if rank == 0:
         total_rows = args.rows * world
@@ -199,7 +204,12 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kernel_ms, "bytes_per_row": b_row,
-                         "model": "B_row=(4+8a)+a(8+8r)+(4+8c)", "a": a, "r": rbar, "c": c},
+                         "model": "B_row=(4+8a)+a(8+8r)+(4+8c)", "a": a, "r": rbar, "c": c,
+                         "traffic_source": "rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per launch, profiles/",
+                         "traffic_GBps": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
+                         "random_line_ceiling_G_per_s": RANDOM_LINE_CEILING / 1e9,
+                         "gathers_G_per_s": gathers_per_s / 1e9,
+                         "frac_of_random_line_ceiling": gathers_per_s / RANDOM_LINE_CEILING},
             "cpu_baseline": cpu,
             "r_setup_s": t_r,
             "r_broadcast_ms": t_bcast * 1e3,
