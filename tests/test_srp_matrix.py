@@ -95,3 +95,11 @@ def test_npz_persistence_roundtrip(tmp_path):
     sm.save_components(str(path), C)
     with pytest.raises(ValueError, match="shape"):
         sm.load_or_fit(str(path), 128, 100_000)
+
+
+def test_gaussian_matrix_matches_sklearn():
+    from sklearn.random_projection import GaussianRandomProjection
+    X = np.zeros((5, 3000), dtype=np.float32)
+    ref = GaussianRandomProjection(n_components=64, random_state=123).fit(X).components_
+    ours = sm.gaussian_random_matrix(64, 3000, random_state=123).astype(np.float32)
+    assert same_bits(ours, ref)
