@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--p", type=int, default=4096)
     ap.add_argument("--dist", choices=["uniform", "powerlaw"], default="uniform")
     ap.add_argument("--order", choices=["scipy", "sorted"], default="scipy")
-    ap.add_argument("--cpu-sample-rows", type=int, default=8_000_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=64_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))

@@ -44,8 +44,8 @@ def dense_project_device(X, C, out=None, compute: str = "fp32"):
         if compute == "bf16":
             Xb = X if X.dtype == torch.bfloat16 else X.to(torch.bfloat16)
             Cb = C if C.dtype == torch.bfloat16 else C.to(torch.bfloat16)
-            y = torch.matmul(Xb, Cb.t(), out_dtype=torch.float32) if _has_out_dtype(torch) else \
-                torch.matmul(Xb, Cb.t()).float()
+            # aten::mm.dtype: bf16 operands, f32 accumulate, f32 result (never rounded to bf16)
+            y = torch.mm(Xb, Cb.t(), out_dtype=torch.float32)
         elif compute == "fp32":
             y = torch.matmul(X.float(), C.float().t())
         elif compute == "fp64":
@@ -58,15 +58,6 @@ def dense_project_device(X, C, out=None, compute: str = "fp32"):
         out.copy_(y)
         return out
     return y
-
-
-def _has_out_dtype(torch):
-    try:
-        a = torch.zeros(1, 1, dtype=torch.bfloat16, device="cuda")
-        torch.matmul(a, a, out_dtype=torch.float32)
-        return True
-    except Exception:  # noqa: BLE001
-        return False
 
 
 class GaussianRandomProjection(_SkGaussianRandomProjection):

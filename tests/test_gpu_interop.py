@@ -22,7 +22,8 @@ print("ok", float(x.sum()))
 
 @pytest.mark.parametrize("lib", ["", "from randomprojection_amd import _native as nat; nat.load(%r)"])
 def test_torch_after_librp(lib):
+    """librp first (implicitly through Projector, or by an explicit load of the in-tree .so)."""
     if lib:
-        lib = lib % (ROOT + "/randomprojection_amd/librp_diag.so")
+        lib = lib % (ROOT + "/randomprojection_amd/librp.so")
     r = subprocess.run([sys.executable, "-c", SCRIPT % (ROOT, lib)], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "ok 0.0" in r.stdout, r.stderr[-2000:]
