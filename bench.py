@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--p", type=int, default=4096)
     ap.add_argument("--dist", choices=["uniform", "powerlaw"], default="uniform")
     ap.add_argument("--order", choices=["scipy", "sorted"], default="scipy")
+    ap.add_argument("--staging", choices=["auto", "on", "off"], default="auto")
+    ap.add_argument("--stage-shift", type=int, default=0, help="2^shift features per staging bucket (0 = auto)")
     ap.add_argument("--cpu-sample-rows", type=int, default=64_000_000)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -114,7 +116,9 @@ def main():
 
     # ---- output buffers sized by an exact first run
     stream = torch.cuda.current_stream(dev).cuda_stream
-    ws = torch.empty(int(nat.load().rp_project_workspace_bytes(P._h, args.rows)), dtype=torch.uint8, device=dev)
+    if args.staging != "auto" or args.stage_shift:
+        P.set_staging(args.staging, args.stage_shift)
+    ws = torch.empty(P.workspace_bytes(args.rows, nnz_a), dtype=torch.uint8, device=dev)
     cap = int(1.3 * nnz_a * P.nnz / P.m) + 1024
     Cj = torch.empty(cap, dtype=torch.int32, device=dev)
     Cx = torch.empty(cap, dtype=torch.float32, device=dev)

@@ -134,17 +134,26 @@ int rp_pack_r_host(int64_t m, int64_t p, const void* indptr, int32_t indptr_type
                    const void* indices, int32_t indices_type, const void* data, int32_t data_type,
                    int32_t layout, rp_projector_info* info, void* buf0, void* buf1, void* buf2);
 
-/* Workspace bytes rp_project_device needs for n_rows (look-back tile states + counters). */
-int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows);
+/* Workspace bytes rp_project_device needs for n_rows rows holding nnz_a entries: look-back tile
+ * states + counters, plus the staged-gather buffers (about 8 bytes per A entry) when the launch
+ * would stage. nnz_a < 0 (unknown): the small look-back part for the worst-case tiling only. */
+int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_t nnz_a);
+
+/* Staged gather (packed R, m < 2^30): the A entries of each tile are bucketed by feature range and
+ * R's descriptors fetched bucket by bucket from an L2-resident slice (three launches instead of one
+ * random 128-B line fill per A entry). mode: -1 auto (large launches over a large R), 0 off, 1 on;
+ * bucket_shift: 2^shift features per bucket (0 = auto, 19). Results are identical either way. */
+int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift);
 
 /* C = A @ R, all device memory, enqueued on `stream` (hipStream_t, NULL = default).
- * workspace: caller device memory of rp_project_workspace_bytes(), or NULL to use the
+ * workspace: caller device memory of workspace_bytes (>= rp_project_workspace_bytes(h, n, -1);
+ * staging runs only if it also covers rp_project_workspace_bytes(h, n, nnz)), or NULL to use the
  * projector's own (then calls on one projector must not run concurrently on different streams).
  * total_nnz: if non-NULL the call synchronizes the stream and stores the exact output nnz;
  * RP_ERR_CAPACITY is returned when it exceeds out->capacity (indptr is still complete).
  * If NULL the call is fully asynchronous (timing loops, graph capture). */
 int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int32_t order,
-                      void* workspace, void* stream, int64_t* total_nnz);
+                      void* workspace, int64_t workspace_bytes, void* stream, int64_t* total_nnz);
 
 /* Host CSR in -> GPU -> exact nnz. The result stays on the device until fetched. */
 int rp_project_host_begin(rp_projector* h, const rp_csr_in* a_host, int32_t order,

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <atomic>
 #include <cstdarg>
 #include <cmath>
@@ -413,13 +414,19 @@ __device__ __forceinline__ uint32_t lds_excl_scan(V* a, uint32_t n, uint32_t* s_
     return total;
 }
 
-template <typename T, typename IP, typename OP, typename OI, typename RL>
+// Staged mode (STAGED, packed R only): stage 1a reads each entry's R descriptor from the staging
+// buffers written by stage_partition_kernel + stage_gather_kernel (below) instead of gathering it
+// from W: S[q] = entry << 20 | column-in-bucket and D[q] = W32 word of that column, for the tile's
+// entries in bucket order (q relative to Ap[0]). Two coalesced 4-byte reads per entry replace one
+// random 128-B line fill.
+template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED>
 __global__ void __launch_bounds__(kBlock)
 spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict__ Ap,
                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
                        OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
                        unsigned long long capacity, Caps caps, int order, Workspace* ws,
-                       unsigned int n_tiles) {
+                       unsigned int n_tiles, const uint32_t* __restrict__ S,
+                       const T* __restrict__ SX, const uint32_t* __restrict__ D) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ uint16_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative, <= cap_a)
     __shared__ uint16_t s_rowS[kBlock + 1];    // row -> first product
@@ -455,20 +462,47 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     if (nnz_t <= caps.cap_a) {  // uniform
         const uint32_t ne = (uint32_t)nnz_t;
         for (int r = tid; r <= nrows; r += kBlock) s_rowptr[r] = (uint16_t)((int64_t)Ap[row0 + r] - ea);
-        // ---- stage 1a: coalesced A entries, one R-descriptor gather per entry
-        uint64_t d[kMaxE];
+        // ---- stage 1a: coalesced A entries, one R-descriptor gather per entry (direct), or the
+        // staged descriptors read in bucket order and scattered to their entries (STAGED).
+        // Registers (kept across the scan below): direct d = the 64-bit W word; staged dw = the
+        // 32-bit W32 word (code 3 = "take W[j]": re-fetched in stage 1c, 2% of KDD2012 entries)
+        // and the entry index, two 16-bit halves per register.
+        constexpr int kD = STAGED ? 1 : kMaxE, kW = STAGED ? kMaxE : 1, kE = STAGED ? kMaxE / 2 : 1;
+        uint64_t d[kD];
+        uint32_t dw[kW];
+        uint32_t eixp[kE];
         T x[kMaxE];
+        const int64_t q0 = STAGED ? ea - (int64_t)Ap[0] : 0;
+        const uint32_t* __restrict__ St = S + q0;   // uniform bases: scalar + 32-bit lane offsets
+        const uint32_t* __restrict__ Dt = D + q0;
+        const T* __restrict__ SXt = SX + q0;
+        const int32_t* __restrict__ Ajt = Aj + ea;
+        const T* __restrict__ Axt = Ax + ea;
 #pragma unroll
         for (int i = 0; i < kMaxE; ++i) {
             const uint32_t e = tid + i * kBlock;
-            d[i] = 0;
             x[i] = T(0);
+            if constexpr (STAGED) {
+                dw[i] = 0;
+                if ((i & 1) == 0) eixp[i >> 1] = 0;
+            } else {
+                d[i] = 0;
+            }
             if (e < ne) {
-                const int32_t j = Aj[ea + e];
-                x[i] = Ax[ea + e];
-                uint32_t cnt;
-                d[i] = r_describe<T>(R, j, cnt);
-                s_eoff[e] = (uint16_t)std::min<uint32_t>(cnt, 0xffffu);
+                uint32_t cnt, ei = e;
+                if constexpr (STAGED) {
+                    x[i] = SXt[e];
+                    const uint32_t w = Dt[e];
+                    ei = St[e] >> 20;
+                    eixp[i >> 1] |= ei << (16 * (i & 1));
+                    dw[i] = w;
+                    cnt = w >> 30;
+                    if (cnt == 3) (void)r_describe<T>(R, (int32_t)(w & 0x3fffffffu), cnt);
+                } else {
+                    x[i] = Axt[e];
+                    d[i] = r_describe<T>(R, Ajt[e], cnt);
+                }
+                s_eoff[ei] = (uint16_t)std::min<uint32_t>(cnt, 0xffffu);
             }
         }
         __syncthreads();
@@ -489,14 +523,25 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
             // ---- stage 1c: every product x*b (one rounding), grouped by row, in (jj, kk) order
 #pragma unroll
             for (int i = 0; i < kMaxE; ++i) {
-                const uint32_t e = tid + i * kBlock;
-                if (e < ne) {
+                if (tid + i * kBlock < ne) {
+                    uint32_t e;
+                    uint64_t de;
+                    if constexpr (STAGED) {
+                        e = (eixp[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+                        const uint32_t code = dw[i] >> 30;
+                        uint32_t cnt;
+                        de = code == 3 ? r_describe<T>(R, (int32_t)(dw[i] & 0x3fffffffu), cnt)
+                                       : (((uint64_t)code << 61) | (uint64_t)(dw[i] & 0x3fffffffu));
+                    } else {
+                        e = tid + i * kBlock;
+                        de = d[i];
+                    }
                     const uint32_t o0 = s_eoff[e], o1 = s_eoff[e + 1];
                     const uint32_t rtag = (uint32_t)s_erow[e] << 16;
                     for (uint32_t t = 0; t < o1 - o0; ++t) {
                         uint32_t col;
                         T v;
-                        r_product<T>(R, mag, d[i], t, x[i], col, v);
+                        r_product<T>(R, mag, de, t, x[i], col, v);
                         s_pkr[o0 + t] = rtag | col;
                         s_pv[o0 + t] = v;
                     }
@@ -584,6 +629,170 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     if (tile == n_tiles - 1 && tid == 0) {
         Cp[n_rows] = (OP)(G + tile_c);
         ws->total = G + tile_c;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Staged gather. Uniform columns over a 437 MB W make every descriptor gather a
+// random 128-B line fill, capped near 55 G lines/s on MI355X whatever the load flavour
+// (profiles/r01_probe_gather_*.json). Staging turns them into L2 hits plus streams:
+//   partition (per tile, coalesced): counting-sort the tile's entries by column bucket
+//             (2^sb features = a W32 slice of 4 * 2^sb bytes) into S (tile-major: the tile's
+//             S range is its own A range), bucket starts into OFFT[bucket][tile];
+//   gather    (per bucket, each XCD on its own buckets so the slice stays in that XCD's 4 MB L2):
+//             D[q] = W32[bucket << sb | S[q] & mask] over every tile's run of the bucket;
+//   the main kernel then reads S and D of its tile with coalesced loads.
+// W32 word of feature j (built from W): bits 30-31 = n if the R row has n <= 2 entries, the low
+// 30 bits then hold W's slots 0-1 unchanged; n = 3 marks "more": the low 30 bits are j itself and
+// the main kernel takes the full word from W (2% of KDD2012 features).
+constexpr int kStageTB = 256;     // tiles per gather workgroup (one per thread for the run bounds)
+constexpr int kStageMaxNB = 256;  // buckets (one per thread in the partition scan)
+constexpr int kStageMap = 16384;  // gather: element -> run map entries (u8) in LDS
+
+__global__ void build_w32_kernel(const uint64_t* __restrict__ W, uint32_t* __restrict__ W32, int64_t m) {
+    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m;
+         j += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t w = W[j];
+        const uint32_t n = (uint32_t)(w >> 61);
+        W32[j] = n <= 2 ? ((n << 30) | (uint32_t)(w & 0x3fffffffu)) : (0xc0000000u | (uint32_t)j);
+    }
+}
+
+
+// one workgroup per tile: bucket histogram (LDS atomics), scan, the tile's entries sorted into LDS,
+// then written to S/SX with coalesced stores; bucket starts go to OFFT[b][t] (adjacent tiles'
+// stores merge in L2), the tile's first entry to TE[t].
+template <typename T, typename IP>
+__global__ void __launch_bounds__(kBlock)
+stage_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                       const T* __restrict__ Ax, int64_t n_rows, Caps caps, unsigned n_tiles,
+                       int sb, int nb, uint32_t ostride, uint32_t* __restrict__ S,
+                       T* __restrict__ SX, uint16_t* __restrict__ OFFT, int64_t* __restrict__ TE) {
+    extern __shared__ __align__(16) unsigned char lds[];  // sorted keys [cap_a] u32, values [cap_a] T
+    __shared__ uint32_t s_hist[kStageMaxNB];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    uint32_t* s_key = reinterpret_cast<uint32_t*>(lds);
+    T* s_val = reinterpret_cast<T*>(lds + 4 * (size_t)caps.cap_a);
+    const int tid = threadIdx.x;
+    const unsigned t = blockIdx.x;
+    const int64_t a0 = (int64_t)Ap[0];
+    const int64_t row0 = (int64_t)t * caps.rpt;
+    const int64_t ea = (int64_t)Ap[row0];
+    const int64_t ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
+    if (tid == 0) TE[t] = ea - a0;
+    if (ne > caps.cap_a) {  // the main kernel's exact slow path reads A itself: empty runs
+        for (int b = tid; b <= nb; b += kBlock) OFFT[(size_t)b * ostride + t] = 0;
+        return;
+    }
+    const uint32_t n = (uint32_t)ne;
+    const uint32_t mask = (1u << sb) - 1u;
+    if (tid < nb) s_hist[tid] = 0;
+    __syncthreads();
+    const int32_t* __restrict__ Ajt = Aj + ea;  // uniform bases, 32-bit lane offsets
+    const T* __restrict__ Axt = Ax + ea;
+    int32_t jj[kMaxE];
+    uint32_t rk[kMaxE];
+#pragma unroll
+    for (int i = 0; i < kMaxE; ++i) {
+        const uint32_t e = tid + i * kBlock;
+        if (e < n) {
+            jj[i] = Ajt[e];
+            rk[i] = atomicAdd(&s_hist[(uint32_t)jj[i] >> sb], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t base = block_excl_scan(tid < nb ? s_hist[tid] : 0u, s_wsum, &tot);
+    if (tid < nb) {
+        s_hist[tid] = base;
+        OFFT[(size_t)tid * ostride + t] = (uint16_t)base;
+    }
+    if (tid == 0) OFFT[(size_t)nb * ostride + t] = (uint16_t)n;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kMaxE; ++i) {
+        const uint32_t e = tid + i * kBlock;
+        if (e < n) {
+            const uint32_t pos = s_hist[(uint32_t)jj[i] >> sb] + rk[i];
+            s_key[pos] = (e << 20) | ((uint32_t)jj[i] & mask);
+            s_val[pos] = Axt[e];
+        }
+    }
+    __syncthreads();
+    uint32_t* __restrict__ St = S + (ea - a0);
+    T* __restrict__ SXt = SX + (ea - a0);
+#pragma unroll
+    for (int i = 0; i < kMaxE; ++i) {
+        const uint32_t e = tid + i * kBlock;
+        if (e < n) {
+            St[e] = s_key[e];
+            SXt[e] = s_val[e];
+        }
+    }
+}
+
+// grid: 8 * ceil(nb / 8) * groups workgroups; workgroup i runs on XCD i % 8 (round-robin dispatch),
+// which takes buckets i % 8, i % 8 + 8, ... in turn, `groups` workgroups of kStageTB tiles each.
+__global__ void __launch_bounds__(kBlock)
+stage_gather_kernel(const uint32_t* __restrict__ W32, const int64_t* __restrict__ TE,
+                    unsigned n_tiles, int sb, int nb, uint32_t ostride, unsigned groups,
+                    const uint16_t* __restrict__ OFFT, const uint32_t* __restrict__ S,
+                    uint32_t* __restrict__ D) {
+    extern __shared__ __align__(16) unsigned char lds[];  // run index of every element (u8)
+    __shared__ uint32_t s_scan[kStageTB + 1];
+    __shared__ int64_t s_base[kStageTB];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    uint8_t* s_run = lds;
+    const int tid = threadIdx.x;
+    const unsigned xcd = blockIdx.x & 7u, k = blockIdx.x >> 3;
+    const unsigned b = xcd + 8u * (k / groups);
+    if (b >= (unsigned)nb) return;  // uniform
+    const unsigned t = (k % groups) * kStageTB + tid;
+    uint32_t len = 0;
+    if (t < n_tiles) {
+        const uint32_t st = OFFT[(size_t)b * ostride + t], en = OFFT[(size_t)(b + 1) * ostride + t];
+        len = en - st;
+        s_base[tid] = TE[t] + st;
+    }
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(len, s_wsum, &total);
+    s_scan[tid] = ex;
+    if (tid == 0) s_scan[kStageTB] = total;
+    // element f of the workgroup belongs to run s_run[f] (an LDS map of the first kStageMap elements)
+    for (uint32_t f = ex; f < std::min<uint32_t>(ex + len, kStageMap); ++f) s_run[f] = (uint8_t)tid;
+    __syncthreads();
+    const uint32_t mask = (1u << sb) - 1u;
+    const uint32_t hi = b << sb;
+    constexpr int kU = 8;  // independent S -> W32 -> D chains in flight per thread
+    for (uint32_t f0 = 0; f0 < total; f0 += kU * kBlock) {
+        int64_t q[kU];
+        uint32_t v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t f = f0 + u * kBlock + tid;
+            q[u] = -1;
+            if (f < total) {
+                uint32_t r;
+                if (f < kStageMap) {
+                    r = s_run[f];
+                } else {  // past the map (a bucket holding most of 256 tiles' entries): search
+                    uint32_t lo = 0, up = kStageTB;
+                    while (up - lo > 1) {
+                        const uint32_t mid = (lo + up) >> 1;
+                        if (s_scan[mid] <= f) lo = mid; else up = mid;
+                    }
+                    r = lo;
+                }
+                q[u] = s_base[r] + (f - s_scan[r]);
+                v[u] = S[q[u]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (q[u] >= 0) v[u] = W32[hi | (v[u] & mask)];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (q[u] >= 0) D[q[u]] = v[u];
     }
 }
 
@@ -735,6 +944,9 @@ struct rp_projector {
     int bs = 0;
     // packed
     DevBuf W, O, spare;  // packed image: W (u64 per feature), O (long-row records); spare unused
+    DevBuf W32;          // staged-gather table derived from W (u32 per feature), m < 2^30 only
+    int stage_mode = -1; // -1 auto, 0 off, 1 on (rp_projector_set_staging)
+    int stage_sb = 0;    // bucket = 2^sb features; 0 = auto
     // generic
     DevBuf Bp, Bj, Bx32, Bx64;
     // internal workspace and host-path staging
@@ -776,23 +988,105 @@ size_t lds_bytes_for(const Caps& c, int value_size, int64_t p) {
     return std::max(L.total, heavy_lds_bytes(p, (size_t)value_size));
 }
 
-template <typename T, typename IP, typename OP, typename OI, typename RL>
-int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
-                 int order, Workspace* ws, unsigned n_tiles, const Caps& caps, size_t lds,
-                 hipStream_t st) {
-    HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL>,
+// Staged-gather plan and workspace carve-up (offsets in bytes from the workspace start):
+//   [Workspace header + look-back states] [TE i64 x tiles] [OFFT u16 x (nb+1) x ostride]
+//   [S u32 x nnz] [D u32 x nnz] [SX value x nnz]   (value size vs: 8 when only sizing)
+struct Plan {
+    Caps caps;
+    int64_t n_tiles = 0;
+    bool staged = false;
+    int sb = 0, nb = 0;
+    uint32_t ostride = 0;
+    size_t head = 0, te = 0, offt = 0, s = 0, d = 0, sx = 0, total = 0;
+};
+
+constexpr bool kStageAuto = false;              // auto picks staging (off until it measures faster)
+constexpr int64_t kStageMinNnz = 1 << 22;      // auto: stage only launches this large
+constexpr int64_t kStageMinTable = 64ll << 20;  // ... and only a W past L2/MALL-friendly sizes
+
+Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_stage = true,
+               int vs = 8) {
+    Plan pl;
+    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    pl.caps = choose_caps(n_rows, nnz_a >= 0 ? nnz_a : n_rows * 11, ppe);
+    pl.n_tiles = n_rows > 0 ? (n_rows + pl.caps.rpt - 1) / pl.caps.rpt : 0;
+    auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
+    pl.head = al(sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(pl.n_tiles, 1));
+    pl.total = pl.head;
+    const bool can = h->layout == RP_LAYOUT_PACKED && h->W32.p && nnz_a > 0 && pl.n_tiles > 0;
+    const bool want = h->stage_mode == 1 ||
+                      (h->stage_mode == -1 && kStageAuto && nnz_a >= kStageMinNnz &&
+                       8 * h->m >= kStageMinTable);
+    if (!(can && want && allow_stage)) return pl;
+    int sb = h->stage_sb > 0 ? h->stage_sb : 19;  // 2 MB W32 slice: stays in an XCD's 4 MB L2
+    auto nbk = [&](int b) { return (int)((h->m + ((int64_t)1 << b) - 1) >> b); };
+    while (h->stage_sb <= 0 && nbk(sb) > kStageMaxNB && sb < 20) ++sb;
+    if (sb < 1 || sb > 20 || nbk(sb) > kStageMaxNB) return pl;
+    pl.staged = true;
+    pl.sb = sb;
+    pl.nb = std::max(nbk(sb), 1);
+    pl.ostride = (uint32_t)((pl.n_tiles + 31) & ~int64_t(31));
+    pl.te = pl.total;
+    pl.offt = pl.te + al(8 * (size_t)pl.n_tiles);
+    pl.s = pl.offt + al(2 * (size_t)(pl.nb + 1) * pl.ostride);
+    pl.d = pl.s + al(4 * (size_t)nnz_a);
+    pl.sx = pl.d + al(4 * (size_t)nnz_a);
+    pl.total = pl.sx + al((size_t)vs * (size_t)nnz_a);
+    return pl;
+}
+
+template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED>
+int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
+                int order, Workspace* ws, unsigned n_tiles, const Caps& caps, size_t lds,
+                hipStream_t st, const uint32_t* S, const T* SX, const uint32_t* D) {
+    HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL>), dim3(n_tiles), dim3(kBlock), lds, st, R, mag, (int)h->p, a->n_rows,
+    hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED>), dim3(n_tiles), dim3(kBlock), lds, st,
+                       R, mag, (int)h->p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
                        (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, caps, order,
-                       ws, n_tiles);
+                       ws, n_tiles, S, SX, D);
     HIP_TRY(hipGetLastError());
     return RP_OK;
 }
 
+template <typename T, typename IP, typename OP, typename OI, typename RL>
+int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
+                 int order, Workspace* ws, unsigned n_tiles, const Plan& pl, size_t lds,
+                 hipStream_t st) {
+    if constexpr (std::is_same<RL, PackedR>::value) {
+        if (pl.staged) {
+            char* base = reinterpret_cast<char*>(ws);
+            int64_t* TE = reinterpret_cast<int64_t*>(base + pl.te);
+            uint16_t* OFFT = reinterpret_cast<uint16_t*>(base + pl.offt);
+            uint32_t* S = reinterpret_cast<uint32_t*>(base + pl.s);
+            uint32_t* D = reinterpret_cast<uint32_t*>(base + pl.d);
+            T* SX = reinterpret_cast<T*>(base + pl.sx);
+            const size_t plds = (4 + sizeof(T)) * (size_t)pl.caps.cap_a;
+            HIP_TRY(hipFuncSetAttribute((const void*)stage_partition_kernel<T, IP>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
+            hipLaunchKernelGGL((stage_partition_kernel<T, IP>), dim3(n_tiles),
+                               dim3(kBlock), plds, st, (const IP*)a->indptr, a->indices,
+                               (const T*)a->data, a->n_rows, pl.caps, n_tiles, pl.sb, pl.nb,
+                               pl.ostride, S, SX, OFFT, TE);
+            HIP_TRY(hipGetLastError());
+            const unsigned groups = (n_tiles + kStageTB - 1) / kStageTB;
+            const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * groups;
+            hipLaunchKernelGGL(stage_gather_kernel, dim3(grid), dim3(kBlock), kStageMap, st,
+                               (const uint32_t*)h->W32.p, (const int64_t*)TE, n_tiles, pl.sb, pl.nb,
+                               pl.ostride, groups, (const uint16_t*)OFFT, (const uint32_t*)S, D);
+            HIP_TRY(hipGetLastError());
+            return launch_main<T, IP, OP, OI, RL, true>(R, mag, h, a, c, order, ws, n_tiles, pl.caps,
+                                                        lds, st, S, SX, D);
+        }
+    }
+    return launch_main<T, IP, OP, OI, RL, false>(R, mag, h, a, c, order, ws, n_tiles, pl.caps, lds,
+                                                 st, nullptr, nullptr, nullptr);
+}
+
 template <typename T, typename RL>
 int dispatch_idx(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
-                 int order, Workspace* ws, unsigned n_tiles, const Caps& caps, size_t lds,
+                 int order, Workspace* ws, unsigned n_tiles, const Plan& caps, size_t lds,
                  hipStream_t st) {
     const bool ip64 = a->indptr_type == RP_I64, op64 = c->indptr_type == RP_I64,
                oi64 = c->indices_type == RP_I64;
@@ -827,7 +1121,8 @@ int ensure_generic_values(rp_projector* h, int T) {
 }
 
 int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
-                        void* workspace, hipStream_t st, int64_t* total_nnz, int64_t nnz_a_hint) {
+                        void* workspace, int64_t workspace_bytes, hipStream_t st,
+                        int64_t* total_nnz, int64_t nnz_a_hint) {
     if (!a || !c) return fail(RP_ERR_INVALID, "NULL operand");
     if (a->n_rows < 0) return fail(RP_ERR_INVALID, "n_rows < 0");
     if (a->data_type != RP_F32 && a->data_type != RP_F64)
@@ -843,23 +1138,29 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
     if (rc) return rc;
     HIP_TRY(hipSetDevice(h->device));
 
-    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
-    const Caps caps = choose_caps(a->n_rows, nnz_a_hint >= 0 ? nnz_a_hint : a->n_rows * 11, ppe);
+    const int vs = dtype_size(a->data_type);
+    Plan plan = make_plan(h, a->n_rows, nnz_a_hint, true, vs);
+    if (workspace) {  // a caller workspace too small for the staging buffers: direct gathers
+        if (workspace_bytes < (int64_t)plan.head)
+            return fail(RP_ERR_INVALID, "workspace of %lld bytes < %zu needed", (long long)workspace_bytes,
+                        plan.head);
+        if (workspace_bytes < (int64_t)plan.total) plan = make_plan(h, a->n_rows, nnz_a_hint, false, vs);
+    }
+    const Caps& caps = plan.caps;
     const size_t lds = lds_bytes_for(caps, dtype_size(a->data_type), h->p);
     if (lds > 160 * 1024 - 4096)
         return fail(RP_ERR_UNSUPPORTED, "p=%lld too large for the LDS accumulator (%zu bytes)",
                     (long long)h->p, lds);
-    const int64_t n_tiles64 = a->n_rows > 0 ? (a->n_rows + caps.rpt - 1) / caps.rpt : 0;
+    const int64_t n_tiles64 = plan.n_tiles;
     if (n_tiles64 >= (int64_t)1 << 31) return fail(RP_ERR_UNSUPPORTED, "too many tiles");
     const unsigned n_tiles = (unsigned)n_tiles64;
-    const size_t ws_bytes = sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(n_tiles64, 1);
-    Workspace* ws = (Workspace*)workspace;
+    Workspace* ws = (Workspace*)workspace;  // caller's: rp_project_workspace_bytes(h, n, nnz) bytes
     if (!ws) {
-        rc = h->ws.ensure(ws_bytes, h->device);
+        rc = h->ws.ensure(plan.total, h->device);
         if (rc) return rc;
         ws = (Workspace*)h->ws.p;
     }
-    HIP_TRY(hipMemsetAsync(ws, 0, ws_bytes, st));
+    HIP_TRY(hipMemsetAsync(ws, 0, plan.head, st));  // header + look-back states only
     if (n_tiles == 0) {
         // empty A: indptr = [0]
         if (c->indptr_type == RP_I64) {
@@ -876,14 +1177,14 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
     if (h->layout == RP_LAYOUT_PACKED) {
         PackedR R{(const uint64_t*)h->W.p, (const uint16_t*)h->O.p};
         rc = a->data_type == RP_F64
-                 ? dispatch_idx<double, PackedR>(R, h->mag, h, a, c, order, ws, n_tiles, caps, lds, st)
-                 : dispatch_idx<float, PackedR>(R, (float)h->mag, h, a, c, order, ws, n_tiles, caps, lds, st);
+                 ? dispatch_idx<double, PackedR>(R, h->mag, h, a, c, order, ws, n_tiles, plan, lds, st)
+                 : dispatch_idx<float, PackedR>(R, (float)h->mag, h, a, c, order, ws, n_tiles, plan, lds, st);
     } else if (a->data_type == RP_F64) {
         GenericR<double> R{(const int32_t*)h->Bp.p, (const uint16_t*)h->Bj.p, (const double*)h->Bx64.p};
-        rc = dispatch_idx<double, GenericR<double>>(R, 0.0, h, a, c, order, ws, n_tiles, caps, lds, st);
+        rc = dispatch_idx<double, GenericR<double>>(R, 0.0, h, a, c, order, ws, n_tiles, plan, lds, st);
     } else {
         GenericR<float> R{(const int32_t*)h->Bp.p, (const uint16_t*)h->Bj.p, (const float*)h->Bx32.p};
-        rc = dispatch_idx<float, GenericR<float>>(R, 0.0f, h, a, c, order, ws, n_tiles, caps, lds, st);
+        rc = dispatch_idx<float, GenericR<float>>(R, 0.0f, h, a, c, order, ws, n_tiles, plan, lds, st);
     }
     if (rc) return rc;
     if (total_nnz) {
@@ -1028,6 +1329,20 @@ int rp_device_count(int* count) {
     return RP_OK;
 }
 
+namespace {
+// the staged-gather table (u32 per feature) derived from the uploaded W
+int build_w32(rp_projector* h) {
+    if (h->layout != RP_LAYOUT_PACKED || h->m <= 0 || h->m >= ((int64_t)1 << 30)) return RP_OK;
+    int rc = h->W32.ensure(4 * (size_t)h->m, h->device);
+    if (rc) return rc;
+    hipLaunchKernelGGL(build_w32_kernel, dim3(2048), dim3(256), 0, nullptr, (const uint64_t*)h->W.p,
+                       (uint32_t*)h->W32.p, h->m);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    return RP_OK;
+}
+}  // namespace
+
 int rp_projector_create(int device, int64_t m, int64_t p, const void* indptr, int32_t indptr_type,
                         const void* indices, int32_t indices_type, const void* data,
                         int32_t data_type, int32_t layout, rp_projector** out) {
@@ -1071,6 +1386,10 @@ int rp_projector_create(int device, int64_t m, int64_t p, const void* indptr, in
             delete h;
             return fail(RP_ERR_HIP, "R upload failed: %s", hipGetErrorString(e));
         }
+    }
+    if ((rc = build_w32(h))) {
+        delete h;
+        return rc;
     }
     *out = h;
     return RP_OK;
@@ -1184,6 +1503,10 @@ int rp_projector_create_from_device(int device, const rp_projector_info* info,
             if (e != hipSuccess) { delete h; return fail(RP_ERR_HIP, "image copy: %s", hipGetErrorString(e)); }
         }
     }
+    if (int rc = build_w32(h)) {
+        delete h;
+        return rc;
+    }
     *out = h;
     return RP_OK;
 }
@@ -1193,14 +1516,33 @@ int rp_projector_destroy(rp_projector* h) {
     return RP_OK;
 }
 
-int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows) {
-    (void)h;
-    const int64_t tiles = n_rows > 0 ? (n_rows + 1 - 1) : 1;  // worst case rpt = 1
-    return (int64_t)sizeof(Workspace) + 8 * tiles;
+int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
+    if (!h || n_rows < 0) return -1;
+    if (nnz_a < 0) {  // unknown nnz: look-back states for the worst case (one row per tile), no staging
+        const int64_t tiles = n_rows > 0 ? n_rows : 1;
+        return (int64_t)((sizeof(Workspace) + 8 * (size_t)tiles + 255) & ~size_t(255));
+    }
+    return (int64_t)make_plan(h, n_rows, nnz_a).total;
+}
+
+int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift) {
+    if (!h) return fail(RP_ERR_INVALID, "NULL projector");
+    if (mode < -1 || mode > 1) return fail(RP_ERR_INVALID, "mode must be -1 (auto), 0 (off) or 1 (on)");
+    if (bucket_shift != 0 && (bucket_shift < 1 || bucket_shift > 20))
+        return fail(RP_ERR_INVALID, "bucket_shift must be 0 (auto) or in [1, 20]");
+    if (mode == 1 && !h->W32.p)
+        return fail(RP_ERR_UNSUPPORTED, "staged gather needs the packed layout and m < 2^30");
+    const int sb = bucket_shift > 0 ? bucket_shift : 20;
+    if (mode == 1 && ((h->m + ((int64_t)1 << sb) - 1) >> sb) > kStageMaxNB)
+        return fail(RP_ERR_INVALID, "m=%lld needs more than %d buckets of 2^%d features", (long long)h->m,
+                    kStageMaxNB, sb);
+    h->stage_mode = mode;
+    h->stage_sb = bucket_shift;
+    return RP_OK;
 }
 
 int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int32_t order,
-                      void* workspace, void* stream, int64_t* total_nnz) {
+                      void* workspace, int64_t workspace_bytes, void* stream, int64_t* total_nnz) {
     if (!h) return fail(RP_ERR_INVALID, "NULL projector");
     if (order != RP_ORDER_SCIPY && order != RP_ORDER_SORTED) return fail(RP_ERR_INVALID, "bad order");
     // nnz(A) for tile sizing: given, or read from the two ends of indptr (tiny D2H)
@@ -1220,7 +1562,8 @@ int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, 
         }
         nnz_a = last - first;
     }
-    return project_device_impl(h, a, c, order, workspace, (hipStream_t)stream, total_nnz, nnz_a);
+    return project_device_impl(h, a, c, order, workspace, workspace_bytes, (hipStream_t)stream,
+                               total_nnz, nnz_a);
 }
 
 int rp_project_host_begin(rp_projector* h, const rp_csr_in* a, int32_t order, rp_result** out,
@@ -1280,7 +1623,7 @@ int rp_project_host_begin(rp_projector* h, const rp_csr_in* a, int32_t order, rp
         }
         rp_csr_out cd{r->cp.p, RP_I64, r->cj.p, RP_I32, r->cx.p, cap};
         int64_t total = 0;
-        rc = project_device_impl(h, &ad, &cd, order, nullptr, nullptr, &total, nnz_a);
+        rc = project_device_impl(h, &ad, &cd, order, nullptr, 0, nullptr, &total, nnz_a);
         if (rc == RP_ERR_CAPACITY && attempt == 0) {
             cap = total;
             continue;

@@ -181,7 +181,8 @@ class Projector:
     # -------------------------------------------------------------------------------- device path
     def project_device(self, Ap, Aj, Ax, Cp, Cj, Cx, order: str = "scipy", stream=0, workspace=None,
                        nnz_a: int = -1, sync: bool = True):
-        """Device-resident product on raw device pointers or torch tensors.
+        """Device-resident product on raw device pointers or torch tensors. ``workspace``: a torch
+        uint8 tensor (or a ``(pointer, bytes)`` pair) of ``workspace_bytes(n, nnz)``, or None.
 
         Returns the exact output nnz when ``sync`` (raises ``RPError`` with code RP_ERR_CAPACITY
         if ``Cj``/``Cx`` are too small), else None (fully asynchronous launch on ``stream``)."""
@@ -200,8 +201,14 @@ class Projector:
         c = nat.CsrOut(p_(Cp), code_(Cp), p_(Cj), code_(Cj), p_(Cx), int(cap))
         total = ctypes.c_int64(0)
         code = nat.RP_ORDER_SORTED if order == "sorted" else nat.RP_ORDER_SCIPY
+        if workspace is None:
+            ws_ptr, ws_bytes = 0, 0
+        elif hasattr(workspace, "data_ptr"):
+            ws_ptr, ws_bytes = int(workspace.data_ptr()), int(workspace.numel() * workspace.element_size())
+        else:
+            ws_ptr, ws_bytes = int(workspace[0]), int(workspace[1])  # (device pointer, bytes)
         rc = self._lib.rp_project_device(self._h, ctypes.byref(a), ctypes.byref(c), code,
-                                         ctypes.c_void_p(p_(workspace) if workspace is not None else 0),
+                                         ctypes.c_void_p(ws_ptr), ws_bytes,
                                          ctypes.c_void_p(stream), ctypes.byref(total) if sync else None)
         if rc == nat.RP_ERR_CAPACITY:
             err = nat.RPError(rc, self._lib.rp_last_error().decode())
@@ -209,6 +216,15 @@ class Projector:
             raise err
         nat.check(rc)
         return int(total.value) if sync else None
+
+    def workspace_bytes(self, n_rows: int, nnz_a: int = -1) -> int:
+        """Device workspace for ``project_device`` on n_rows rows / nnz_a entries (staging included)."""
+        return int(self._lib.rp_project_workspace_bytes(self._h, int(n_rows), int(nnz_a)))
+
+    def set_staging(self, mode: str = "auto", bucket_shift: int = 0):
+        """Staged gather: "auto", "off" or "on" (identical results)."""
+        code = {"auto": -1, "off": 0, "on": 1}[mode]
+        nat.check(self._lib.rp_projector_set_staging(self._h, code, int(bucket_shift)))
 
     def __repr__(self):
         return f"Projector(m={self.m}, p={self.p}, nnz={self.nnz}, layout={self.layout}, device={self.device})"

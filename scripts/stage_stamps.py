@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=20_000_000)
     ap.add_argument("--dist", default="uniform")
+    ap.add_argument("--staging", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stamps.json"))
     args = ap.parse_args()
 
@@ -33,6 +34,7 @@ def main():
 
     R = sm.projection_operand(sm.sparse_random_matrix(4096, sm.KDD_M, random_state=123))
     P = Projector(R)
+    P.set_staging(args.staging)
     Ap, Aj, Ax = synth.kdd_rows_device(args.rows, sm.KDD_M, seed=7, dist=args.dist)
     n_tiles = (args.rows + 255) // 256
     stamps = torch.zeros(n_tiles * 8, dtype=torch.int64, device="cuda")
@@ -47,7 +49,7 @@ def main():
     torch.cuda.synchronize()
     st = stamps.view(n_tiles, 8).cpu().numpy().astype(np.int64)
     t0 = st[:, 0].min()
-    names = ["gather(1a)", "scan(1b)", "products(1c)", "accumulate(2)", "scan+lookback(3a)", "write(3b)"]
+    names = ["gather-or-staged-read(1a)", "scan(1b)", "products(1c)", "accumulate(2)", "scan+lookback(3a)", "write(3b)"]
     res = {"tiles": int(n_tiles), "heavy_tiles": int((st[:, 7] > 0).sum())}
     ok = st[:, 6] > 0
     for k, nm in enumerate(names):

@@ -1,0 +1,119 @@
+"""Staged gather: bucketed descriptor fetch + coalesced main kernel. Results must be
+bit-identical to the direct-gather kernel and to the oracle (CPU restatement of scipy csr_matmat)
+for every bucket width, order, dtype, tile shape and workspace arrangement."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import smmp
+from randomprojection_amd import Projector, srp_matrix as sm
+from test_gpu_parity import assert_same_csr, kdd_like, oracle_product
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def R2m():
+    return sm.projection_operand(sm.sparse_random_matrix(4096, 2_000_000, random_state=123))
+
+
+def _staged(R, shift, **kw):
+    P = Projector(R, **kw)
+    P.set_staging("on", shift)
+    return P
+
+
+@pytest.mark.parametrize("shift", [13, 16, 19])
+@pytest.mark.parametrize("powerlaw", [False, True])
+def test_staged_kdd_vs_oracle(R2m, shift, powerlaw):
+    rng = np.random.default_rng(100 + shift + powerlaw)
+    A = kdd_like(rng, 60_000, R2m.shape[0], powerlaw=powerlaw, values="normal")
+    P = _staged(R2m, shift)
+    assert P.workspace_bytes(A.shape[0], A.nnz) >= 8 * A.nnz  # S + D staging buffers
+    want = oracle_product(A, R2m)
+    assert_same_csr(P.matmul(A), *want)
+    Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
+    assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
+
+
+def test_staged_f64_and_heavy_tiles():
+    """f64 compute, rows past the LDS caps (exact slow path, no staged runs) mixed with short rows."""
+    rng = np.random.default_rng(21)
+    m, p = 5000, 64
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123), dtype=np.float64)
+    parts = [kdd_like(rng, 300, m, mean=10, values="normal", dtype=np.float64),
+             kdd_like(rng, 3, m, mean=900, values="normal", dtype=np.float64, cap=m),
+             kdd_like(rng, 20, m, mean=300, values="normal", dtype=np.float64),
+             sp.csr_matrix((50, m), dtype=np.float64),
+             kdd_like(rng, 400, m, mean=3, values="normal", dtype=np.float64)]
+    A = sp.vstack(parts).tocsr()
+    for shift in (5, 8, 12):
+        P = _staged(R, shift)
+        for order in ("scipy", "sorted"):
+            Cp, Cj, Cx = oracle_product(A, R)
+            if order == "sorted":
+                Cj, Cx = smmp.sorted_rows(Cp, Cj, Cx)
+            assert_same_csr(P.matmul(A, order=order), Cp, Cj, Cx)
+
+
+def test_staged_equals_direct_cfg4_shape():
+    """100 nnz/row power-law rows over p=1024 (config 4 shape, m scaled to 2M)."""
+    rng = np.random.default_rng(4)
+    m, p = 2_000_000, 1024
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    A = kdd_like(rng, 4000, m, mean=99, powerlaw=True, values="normal")
+    direct = Projector(R)
+    direct.set_staging("off")
+    Cd = direct.matmul(A)
+    Cs = _staged(R, 15).matmul(A)
+    assert_same_csr(Cs, Cd.indptr, Cd.indices, Cd.data)
+    assert_same_csr(Cs, *oracle_product(A, R))
+
+
+def test_staged_device_path_workspace_and_offset_indptr(R2m):
+    """Caller workspace: large enough -> staged; too small for staging -> direct; indptr[0] != 0."""
+    import torch
+
+    rng = np.random.default_rng(8)
+    A = kdd_like(rng, 30_000, R2m.shape[0], values="normal")
+    P = _staged(R2m, 17)
+    dev = torch.device("cuda", 0)
+    want = oracle_product(A, R2m)
+    skip = 1000  # rows [skip:] through an indptr whose first value is A.indptr[skip] (not 0)
+    sub = A[skip:]
+    want_sub = oracle_product(sub, R2m)
+    for small in (False, True):
+        for base in (0, skip):
+            Ap = torch.as_tensor(A.indptr[base:].astype(np.int64), device=dev)
+            Aj = torch.as_tensor(A.indices, device=dev)
+            Ax = torch.as_tensor(A.data, device=dev)
+            n = A.shape[0] - base
+            nnz = int(A.indptr[-1] - A.indptr[base])
+            full = P.workspace_bytes(n, nnz)
+            ws = torch.empty(P.workspace_bytes(n) if small else full, dtype=torch.uint8, device=dev)
+            cap = 4 * nnz  # >= output nnz for this R (2.9 products per entry)
+            Cp = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            Cj = torch.empty(cap, dtype=torch.int32, device=dev)
+            Cx = torch.empty(cap, dtype=torch.float32, device=dev)
+            k = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, workspace=ws, nnz_a=nnz)
+            torch.cuda.synchronize()
+            ref = want if base == 0 else want_sub
+            got = sp.csr_matrix((Cx[:k].cpu().numpy(), Cj[:k].cpu().numpy(), Cp.cpu().numpy()),
+                                shape=(n, R2m.shape[1]))
+            assert_same_csr(got, *ref)
+
+
+def test_staging_arguments():
+    from randomprojection_amd import _native as nat
+
+    R = sm.projection_operand(sm.sparse_random_matrix(64, 100_000, random_state=123))
+    P = Projector(R)
+    with pytest.raises(nat.RPError):
+        P.set_staging("on", 8)       # 391 buckets > 256
+    with pytest.raises(nat.RPError):
+        P.set_staging("on", 21)
+    G = Projector(R, layout="generic")
+    with pytest.raises(nat.RPError):
+        G.set_staging("on")
+    G.set_staging("off")
+    P.set_staging("auto")
