@@ -27,6 +27,23 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 RANDOM_LINE_CEILING = 55e9  # random 128-B line fills/s, measured (scripts/probes/gather_probe*.hip)
 
 
+# BASELINE.json configs: [1] KDD2012 train on one GPU (the headline); [3] the power-law stress shape
+CONFIGS = {
+    "kdd": {"rows": 119_705_032, "m": 54_686_452, "p": 4096, "dist": "uniform", "mean_extra": 10.0,
+            "cpu_sample_rows": 64_000_000,
+            "metric": "rows/sec projected (whole node), KDD2012 54.7M->4096 dims; achieved HBM GB/s",
+            "workload": "configs[1]: KDD2012 train {rows} rows x {m} -> {p} per GPU, device-resident CSR in/out",
+            "data": "synthetic KDD2012-shaped rows ({dist} columns, 1+Poisson(10) nnz/row, values 1.0), "
+                    "R = SparseRandomProjection({p}, random_state=123) regenerated bit-identically"},
+    "cfg4": {"rows": 200_000_000, "m": 10_000_000, "p": 1024, "dist": "powerlaw", "mean_extra": -100.0,
+             "cpu_sample_rows": 4_000_000,
+             "metric": "rows/sec projected, synthetic power-law 200M x 10M (100 nnz/row) -> 1024; achieved HBM GB/s",
+             "workload": "configs[3]: power-law {rows} rows x {m}, 100 nnz/row -> {p} per GPU, device-resident CSR in/out",
+             "data": "synthetic power-law rows ({dist} columns: Zipf(1.1) over a fixed permutation, exactly 100 "
+                     "distinct nnz/row, values 1.0), R = SparseRandomProjection({p}, random_state=123)"},
+}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -39,21 +56,28 @@ def algorithmic_bytes_per_row(a, rbar, c):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", choices=["kdd", "cfg4"], default="kdd",
+                    help="kdd: BASELINE configs[1] (default); cfg4: configs[3], 200M x 10M power-law rows, "
+                         "exactly 100 nnz/row -> 1024")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=119_705_032)
-    ap.add_argument("--m", type=int, default=54_686_452)
-    ap.add_argument("--p", type=int, default=4096)
-    ap.add_argument("--dist", choices=["uniform", "powerlaw"], default="uniform")
+    ap.add_argument("--rows", type=int, default=None)
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--p", type=int, default=None)
+    ap.add_argument("--dist", choices=["uniform", "powerlaw"], default=None)
     ap.add_argument("--order", choices=["scipy", "sorted"], default="scipy")
     ap.add_argument("--staging", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--stage-shift", type=int, default=0, help="2^shift features per staging bucket (0 = auto)")
-    ap.add_argument("--cpu-sample-rows", type=int, default=64_000_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=None)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    for k in ("rows", "m", "p", "dist", "cpu_sample_rows"):
+        if getattr(args, k) is None:
+            setattr(args, k, cfg[k])
 
     import torch
     import torch.distributed as dist
@@ -109,7 +133,8 @@ def main():
 
     # ---- A: this rank's synthetic shard, generated in HBM
     t0 = time.perf_counter()
-    Ap, Aj, Ax = synth.kdd_rows_device(args.rows, args.m, seed=2012 + rank, dist=args.dist, device=local)
+    Ap, Aj, Ax = synth.kdd_rows_device(args.rows, args.m, seed=2012 + rank, dist=args.dist, device=local,
+                                       mean_extra=cfg["mean_extra"])
     torch.cuda.synchronize()
     nnz_a = int(Aj.numel())
     log(f"[rank {rank}] A: {args.rows} rows, nnz={nnz_a} ({time.perf_counter() - t0:.1f}s)")
@@ -188,7 +213,7 @@ def main():
     if rank == 0:
         total_rows = args.rows * world
         out = {
-            "metric": "rows/sec projected (whole node), KDD2012 54.7M->4096 dims; achieved HBM GB/s",
+            "metric": cfg["metric"],
             "value": total_rows / (t_max / args.steps),
             "unit": "rows/s",
             "n_gpus": world,
@@ -199,10 +224,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic KDD2012-shaped rows ({args.dist} columns, 1+Poisson(10) nnz/row, values 1.0), "
-                    "R = SparseRandomProjection(4096, random_state=123) regenerated bit-identically",
-            "config": {"workload": f"configs[1]: KDD2012 train {args.rows} rows x {args.m} -> {args.p} "
-                                   f"per GPU, device-resident CSR in/out",
+            "data": cfg["data"].format(dist=args.dist, p=args.p),
+            "config": {"workload": cfg["workload"].format(rows=args.rows, m=args.m, p=args.p),
                        "rows_per_gpu": args.rows, "m": args.m, "p": args.p, "nnz_in": nnz_a, "nnz_out": nnz_c,
                        "order": args.order, "r_layout": P.layout, "parallelism": f"row-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -164,7 +164,8 @@ int rp_result_fetch(rp_result* r, void* indptr, int32_t indptr_type, void* indic
                     int32_t indices_type, void* data);
 int rp_result_free(rp_result* r);
 
-/* Synthetic rows on the device: per-row nnz = 1 + Poisson(mean_extra) (capped at max_row_nnz),
+/* Synthetic rows on the device: per-row nnz = 1 + Poisson(mean_extra), or exactly -mean_extra
+ * when mean_extra < 0 (capped at max_row_nnz),
  * distinct ascending columns in [0, m) — uniform (dist 0) or power-law Zipf(s) over a fixed
  * permutation without replacement (dist 1) — values 1.0f. Two calls: first with indices == NULL
  * to fill indptr (int32 or int64) and get the nnz, then with indices/data of that size. */

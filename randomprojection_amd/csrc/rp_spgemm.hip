@@ -822,6 +822,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 __device__ __forceinline__ double u01(uint64_t h) { return ((h >> 11) + 0.5) * (1.0 / 9007199254740992.0); }
 
 __device__ int synth_count(uint64_t seed, int64_t row, double lam, int cap) {
+    if (lam < 0) return std::min((int)(-lam + 0.5), cap);  // fixed count (configs[3]: 100 per row)
     // 1 + Poisson(lam) by inversion
     const double u = u01(mix64(seed ^ mix64((uint64_t)row * 2 + 1)));
     double pk = exp(-lam), cdf = pk;
