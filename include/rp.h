@@ -147,8 +147,9 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
 
 /* C = A @ R, all device memory, enqueued on `stream` (hipStream_t, NULL = default).
  * workspace: caller device memory of workspace_bytes (>= rp_project_workspace_bytes(h, n, -1);
- * staging runs only if it also covers rp_project_workspace_bytes(h, n, nnz)), or NULL to use the
- * projector's own (then calls on one projector must not run concurrently on different streams).
+ * the full rp_project_workspace_bytes(h, n, nnz) also enables deferred tile output (no tile
+ * waits on its predecessors) and staging), or NULL to use the projector's own (then calls on one
+ * projector must not run concurrently on different streams).
  * total_nnz: if non-NULL the call synchronizes the stream and stores the exact output nnz;
  * RP_ERR_CAPACITY is returned when it exceeds out->capacity (indptr is still complete).
  * If NULL the call is fully asynchronous (timing loops, graph capture). */

@@ -9,6 +9,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librp.so")
+# timing experiments only (scripts/): RP_LIB names a diagnostic build to load instead
+_LIB_OVERRIDE = os.environ.get("RP_LIB")
 
 RP_OK, RP_ERR_INVALID, RP_ERR_HIP, RP_ERR_CAPACITY, RP_ERR_UNSUPPORTED, RP_ERR_NOMEM, RP_ERR_TIMEOUT = range(7)
 RP_I32, RP_I64, RP_F32, RP_F64 = 1, 2, 3, 4
@@ -64,11 +66,13 @@ class CsrOut(ctypes.Structure):
 _lib = None
 
 
-def load(path: str = LIB_PATH):
+def load(path: str = None):
     """Load librp.so (built by ``randomprojection_amd.build`` / ``__graft_entry__.build``)."""
     global _lib
     if _lib is not None:
         return _lib
+    if path is None:
+        path = _LIB_OVERRIDE or LIB_PATH
     if not os.path.exists(path):
         raise NativeUnavailable(
             f"{path} is missing: build it with `python -m randomprojection_amd.build` "

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 #include <atomic>
 #include <cstdarg>
@@ -55,6 +56,9 @@ constexpr long kSpinLimit = 1l << 27;     // bounded waits (with s_sleep): secon
 
 // Diagnostic builds (-DRP_STAMPS, librp_diag.so only): thread 0 of each tile records
 // s_memrealtime (100 MHz) at stage boundaries into g_stamps[tile * 8 + k]. Never in librp.so.
+#ifndef RP_EXP
+#define RP_EXP 0  // timing experiments (scripts only): 1 no stage 2, 2 no products, 3 no look-back, 4 no writes
+#endif
 #ifdef RP_STAMPS
 __device__ unsigned long long* g_stamps;
 #define STAMP(k)                                                                                  \
@@ -72,8 +76,25 @@ struct Workspace {              // device memory header; tile states follow at +
     unsigned int tile_counter;
     unsigned int error;
     unsigned long long total;
-    unsigned long long pad[6];
+    unsigned int n_deferred;    // tiles that parked their output in a temp slot (see defer below)
+    unsigned int pad0;
+    unsigned long long pad[5];
 };
+
+// Deferred output: a tile whose exclusive prefix is not published within
+// `defer_polls` look-back polls does not wait: it parks its finished output in its temp slot
+// (row offsets + entries in final order), leaves its aggregate published, appends itself to the
+// deferred list and exits; defer_copy_kernel later resolves its prefix (every state is final
+// then) and copies the slot to its place. Waiting tiles hold LDS and waves idle: measured 7.6 ms
+// of 32.9 on configs[1] (direct gathers).
+struct DeferSpace {
+    unsigned int* list;     // n_tiles
+    unsigned char* slots;   // n_tiles x slot_bytes
+    size_t slot_bytes;
+};
+__host__ __device__ inline size_t defer_slot_bytes(int cap_p, int rpt, size_t vs) {
+    return ((2 * (size_t)(rpt + 1) + 15) & ~size_t(15)) + (((4 + vs) * (size_t)cap_p + 255) & ~size_t(255));
+}
 
 // ------------------------------------------------------------------------------------------
 // R layouts
@@ -199,15 +220,19 @@ __device__ unsigned long long wave_sum_u64(unsigned long long v) {
     return v;
 }
 
+// max_polls < 0: wait (bounded by kSpinLimit); otherwise give up after max_polls unsuccessful
+// polls, return ~0ull and leave only the aggregate published. publish_agg = false: the aggregate
+// is already there (defer_copy_kernel).
 __device__ unsigned long long lookback_wave(unsigned long long* states, unsigned int tile,
-                                            unsigned long long agg, Workspace* ws) {
+                                            unsigned long long agg, Workspace* ws,
+                                            long max_polls = -1, bool publish_agg = true) {
     const int lane = threadIdx.x & 63;
     if (tile == 0) {
         if (lane == 0)
             __hip_atomic_store(&states[0], kFlagP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0;
     }
-    if (lane == 0)
+    if (lane == 0 && publish_agg)
         __hip_atomic_store(&states[tile], kFlagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned long long excl = 0;
     long base = (long)tile - 1;  // nearest predecessor not yet summed
@@ -227,6 +252,7 @@ __device__ unsigned long long lookback_wave(unsigned long long* states, unsigned
             base -= 64;
             continue;
         }
+        if (max_polls >= 0 && spins >= max_polls) return ~0ull;  // defer: aggregate stays published
         if (++spins > kSpinLimit) {
             if (lane == 0) atomicOr(&ws->error, 1u);
             break;
@@ -426,7 +452,8 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                        OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
                        unsigned long long capacity, Caps caps, int order, Workspace* ws,
                        unsigned int n_tiles, const uint32_t* __restrict__ S,
-                       const T* __restrict__ SX, const uint32_t* __restrict__ D) {
+                       const T* __restrict__ SX, const uint32_t* __restrict__ D,
+                       DeferSpace dfr, int defer_polls) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ uint16_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative, <= cap_a)
     __shared__ uint16_t s_rowS[kBlock + 1];    // row -> first product
@@ -538,7 +565,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     }
                     const uint32_t o0 = s_eoff[e], o1 = s_eoff[e + 1];
                     const uint32_t rtag = (uint32_t)s_erow[e] << 16;
-                    for (uint32_t t = 0; t < o1 - o0; ++t) {
+                    for (uint32_t t = 0; t < o1 - o0 && RP_EXP != 2; ++t) {
                         uint32_t col;
                         T v;
                         r_product<T>(R, mag, de, t, x[i], col, v);
@@ -553,7 +580,8 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 // ---- stage 2: flat over products. A product leads its column group if no earlier
                 // product of its row has that column (= scipy's first touch); the leader sums the
                 // group in sequence order starting from +0 (scipy: sums[k] = 0, then +=).
-                for (uint32_t q = tid; q < P_t; q += kBlock) {
+                for (uint32_t q = tid; q < P_t && (RP_EXP == 1 || RP_EXP == 2); q += kBlock) s_rank[q] = 1;
+                for (uint32_t q = tid; q < P_t && RP_EXP != 1 && RP_EXP != 2; q += kBlock) {
                     const uint32_t kr = s_pkr[q];
                     const uint32_t r = kr >> 16;
                     const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
@@ -574,14 +602,31 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 // ---- stage 3: ranks of kept entries = tile-local output positions; look-back
                 const uint32_t tile_c = lds_excl_scan(s_rank, P_t, s_wsum);
                 if (tid < 64) {
-                    const unsigned long long g = lookback_wave(states, tile, tile_c, ws);
+                    const unsigned long long g =
+                        RP_EXP == 3 ? 0ull : lookback_wave(states, tile, tile_c, ws, defer_polls);
                     if (tid == 0) s_off = g;
                 }
                 __syncthreads();
                 STAMP(5);
-                const unsigned long long G = s_off;
-                if (tid < nrows) Cp[row0 + tid] = (OP)(G + s_rank[s_rowS[tid]]);
-                if (G + tile_c <= capacity) {
+                const bool deferred = s_off == ~0ull;  // uniform
+                const unsigned long long G = deferred ? 0ull : s_off;
+                // deferred: entries go to the tile's temp slot at their tile-local positions and the
+                // row offsets to the slot header; defer_copy_kernel adds the prefix later
+                unsigned char* slot = dfr.slots + (size_t)tile * dfr.slot_bytes;
+                OI* __restrict__ Cjw = Cj;
+                T* __restrict__ Cxw = Cx;
+                if (deferred) {
+                    const size_t hdr = (2 * (size_t)(caps.rpt + 1) + 15) & ~size_t(15);
+                    Cjw = reinterpret_cast<OI*>(slot + hdr);  // u32 columns (OI-typed view, see copy)
+                    Cxw = reinterpret_cast<T*>(slot + hdr + 4 * (size_t)caps.cap_p);
+                    uint16_t* ro = reinterpret_cast<uint16_t*>(slot);
+                    if (tid < nrows) ro[tid] = s_rank[s_rowS[tid]];
+                    if (tid == 0) ro[nrows] = (uint16_t)tile_c;
+                    if (tid == 0) dfr.list[atomicAdd(&ws->n_deferred, 1u)] = tile;
+                } else if (tid < nrows) {
+                    Cp[row0 + tid] = (OP)(G + s_rank[s_rowS[tid]]);
+                }
+                if ((deferred || G + tile_c <= capacity) && RP_EXP != 4) {
                     // kept leaders write straight into the tile's contiguous output range
                     for (uint32_t q = tid; q < P_t; q += kBlock) {
                         const uint32_t rk = s_rank[q];
@@ -596,11 +641,16 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                         } else {
                             pos += s_rank[re] - 1 - rk;  // reverse first-touch order
                         }
-                        Cj[G + pos] = (OI)(kr & 0xffffu);
-                        Cx[G + pos] = s_pv[q];
+                        if (deferred) {
+                            reinterpret_cast<uint32_t*>(Cjw)[pos] = kr & 0xffffu;
+                            Cxw[pos] = s_pv[q];
+                        } else {
+                            Cj[G + pos] = (OI)(kr & 0xffffu);
+                            Cx[G + pos] = s_pv[q];
+                        }
                     }
                 }
-                if (tile == n_tiles - 1 && tid == 0) {
+                if (!deferred && tile == n_tiles - 1 && tid == 0) {
                     Cp[n_rows] = (OP)(G + tile_c);
                     ws->total = G + tile_c;
                 }
@@ -793,6 +843,48 @@ stage_gather_kernel(const uint32_t* __restrict__ W32, const int64_t* __restrict_
 #pragma unroll
         for (int u = 0; u < kU; ++u)
             if (q[u] >= 0) D[q[u]] = v[u];
+    }
+}
+
+// Deferred tiles: prefix from the (now final) look-back states, then the parked slot is copied to
+// its place. Grid-stride over the deferred list; every state is published when this runs.
+template <typename T, typename OP, typename OI>
+__global__ void __launch_bounds__(kBlock)
+defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsigned n_tiles,
+                  OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
+                  unsigned long long capacity) {
+    __shared__ unsigned long long s_g;
+    unsigned long long* states = reinterpret_cast<unsigned long long*>(ws + 1);
+    const unsigned nd = ws->n_deferred;
+    const int tid = threadIdx.x;
+    const size_t hdr = (2 * (size_t)(caps.rpt + 1) + 15) & ~size_t(15);
+    for (unsigned i = blockIdx.x; i < nd; i += gridDim.x) {
+        const unsigned tile = dfr.list[i];
+        const unsigned char* slot = dfr.slots + (size_t)tile * dfr.slot_bytes;
+        const uint16_t* ro = reinterpret_cast<const uint16_t*>(slot);
+        const int64_t row0 = (int64_t)tile * caps.rpt;
+        const int nrows = (int)std::min<int64_t>(caps.rpt, n_rows - row0);
+        const uint32_t cnt = ro[nrows];
+        if (tid < 64) {
+            const unsigned long long g = lookback_wave(states, tile, cnt, ws, -1, false);
+            if (tid == 0) s_g = g;
+        }
+        __syncthreads();
+        const unsigned long long G = s_g;
+        for (int r = tid; r < nrows; r += kBlock) Cp[row0 + r] = (OP)(G + ro[r]);
+        if (G + cnt <= capacity) {
+            const uint32_t* cj = reinterpret_cast<const uint32_t*>(slot + hdr);
+            const T* cx = reinterpret_cast<const T*>(slot + hdr + 4 * (size_t)caps.cap_p);
+            for (uint32_t q = tid; q < cnt; q += kBlock) {
+                Cj[G + q] = (OI)cj[q];
+                Cx[G + q] = cx[q];
+            }
+        }
+        if (tile == n_tiles - 1 && tid == 0) {
+            Cp[n_rows] = (OP)(G + cnt);
+            ws->total = G + cnt;
+        }
+        __syncthreads();
     }
 }
 
@@ -996,17 +1088,20 @@ struct Plan {
     Caps caps;
     int64_t n_tiles = 0;
     bool staged = false;
+    bool defer = false;
     int sb = 0, nb = 0;
     uint32_t ostride = 0;
-    size_t head = 0, te = 0, offt = 0, s = 0, d = 0, sx = 0, total = 0;
+    size_t head = 0, dlist = 0, slots = 0, slot_bytes = 0, te = 0, offt = 0, s = 0, d = 0, sx = 0;
+    size_t total = 0;
 };
 
+constexpr int kDeferPolls = 2;                 // look-back polls before a tile defers its output
 constexpr bool kStageAuto = false;              // auto picks staging (off until it measures faster)
 constexpr int64_t kStageMinNnz = 1 << 22;      // auto: stage only launches this large
 constexpr int64_t kStageMinTable = 64ll << 20;  // ... and only a W past L2/MALL-friendly sizes
 
 Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_stage = true,
-               int vs = 8) {
+               int vs = 8, bool allow_defer = true) {
     Plan pl;
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
     pl.caps = choose_caps(n_rows, nnz_a >= 0 ? nnz_a : n_rows * 11, ppe);
@@ -1014,6 +1109,13 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
     auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
     pl.head = al(sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(pl.n_tiles, 1));
     pl.total = pl.head;
+    if (pl.n_tiles > 0 && allow_defer) {  // deferred-output list and temp slots
+        pl.defer = true;
+        pl.dlist = pl.total;
+        pl.slot_bytes = defer_slot_bytes(pl.caps.cap_p, pl.caps.rpt, (size_t)vs);
+        pl.slots = pl.dlist + al(4 * (size_t)pl.n_tiles);
+        pl.total = pl.slots + pl.slot_bytes * (size_t)pl.n_tiles;
+    }
     const bool can = h->layout == RP_LAYOUT_PACKED && h->W32.p && nnz_a > 0 && pl.n_tiles > 0;
     const bool want = h->stage_mode == 1 ||
                       (h->stage_mode == -1 && kStageAuto && nnz_a >= kStageMinNnz &&
@@ -1036,18 +1138,32 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
     return pl;
 }
 
+int defer_polls_setting() {
+    const char* e = getenv("RP_DEFER_POLLS");  // tests and tuning: -1 never defer, 0 defer at once
+    return e ? atoi(e) : kDeferPolls;
+}
+
 template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED>
 int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
-                int order, Workspace* ws, unsigned n_tiles, const Caps& caps, size_t lds,
+                int order, Workspace* ws, unsigned n_tiles, const Plan& pl, size_t lds,
                 hipStream_t st, const uint32_t* S, const T* SX, const uint32_t* D) {
     HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    char* base = reinterpret_cast<char*>(ws);
+    DeferSpace dfr{reinterpret_cast<unsigned int*>(base + pl.dlist),
+                   reinterpret_cast<unsigned char*>(base + pl.slots), pl.slot_bytes};
     hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED>), dim3(n_tiles), dim3(kBlock), lds, st,
                        R, mag, (int)h->p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
-                       (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, caps, order,
-                       ws, n_tiles, S, SX, D);
+                       (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order,
+                       ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting() : -1);
     HIP_TRY(hipGetLastError());
+    if (pl.defer) {
+        hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, 4096u)), dim3(kBlock), 0,
+                           st, dfr, ws, pl.caps, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices,
+                           (T*)c->data, (unsigned long long)c->capacity);
+        HIP_TRY(hipGetLastError());
+    }
     return RP_OK;
 }
 
@@ -1077,11 +1193,11 @@ int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const 
                                (const uint32_t*)h->W32.p, (const int64_t*)TE, n_tiles, pl.sb, pl.nb,
                                pl.ostride, groups, (const uint16_t*)OFFT, (const uint32_t*)S, D);
             HIP_TRY(hipGetLastError());
-            return launch_main<T, IP, OP, OI, RL, true>(R, mag, h, a, c, order, ws, n_tiles, pl.caps,
+            return launch_main<T, IP, OP, OI, RL, true>(R, mag, h, a, c, order, ws, n_tiles, pl,
                                                         lds, st, S, SX, D);
         }
     }
-    return launch_main<T, IP, OP, OI, RL, false>(R, mag, h, a, c, order, ws, n_tiles, pl.caps, lds,
+    return launch_main<T, IP, OP, OI, RL, false>(R, mag, h, a, c, order, ws, n_tiles, pl, lds,
                                                  st, nullptr, nullptr, nullptr);
 }
 
@@ -1141,11 +1257,13 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
 
     const int vs = dtype_size(a->data_type);
     Plan plan = make_plan(h, a->n_rows, nnz_a_hint, true, vs);
-    if (workspace) {  // a caller workspace too small for the staging buffers: direct gathers
+    if (workspace) {  // a smaller caller workspace: no staging, then no deferred output either
         if (workspace_bytes < (int64_t)plan.head)
             return fail(RP_ERR_INVALID, "workspace of %lld bytes < %zu needed", (long long)workspace_bytes,
                         plan.head);
         if (workspace_bytes < (int64_t)plan.total) plan = make_plan(h, a->n_rows, nnz_a_hint, false, vs);
+        if (workspace_bytes < (int64_t)plan.total)
+            plan = make_plan(h, a->n_rows, nnz_a_hint, false, vs, false);
     }
     const Caps& caps = plan.caps;
     const size_t lds = lds_bytes_for(caps, dtype_size(a->data_type), h->p);
@@ -1519,7 +1637,7 @@ int rp_projector_destroy(rp_projector* h) {
 
 int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
     if (!h || n_rows < 0) return -1;
-    if (nnz_a < 0) {  // unknown nnz: look-back states for the worst case (one row per tile), no staging
+    if (nnz_a < 0) {  // unknown nnz: look-back states for the worst case (one row per tile) only
         const int64_t tiles = n_rows > 0 ? n_rows : 1;
         return (int64_t)((sizeof(Workspace) + 8 * (size_t)tiles + 255) & ~size_t(255));
     }

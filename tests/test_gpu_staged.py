@@ -117,3 +117,21 @@ def test_staging_arguments():
         G.set_staging("on")
     G.set_staging("off")
     P.set_staging("auto")
+
+
+@pytest.mark.parametrize("polls", ["0", "-1", "3"])
+@pytest.mark.parametrize("staged", [False, True])
+def test_deferred_output_tiles(R2m, polls, staged, monkeypatch):
+    """Tiles that park their output (RP_DEFER_POLLS=0: nearly all) and tiles that wait (-1) give
+    the same bits; mixed with heavy tiles, empty rows, both orders."""
+    monkeypatch.setenv("RP_DEFER_POLLS", polls)
+    rng = np.random.default_rng(31)
+    m = R2m.shape[0]
+    A = sp.vstack([kdd_like(rng, 20_000, m, values="normal"), sp.csr_matrix((300, m), dtype=np.float32),
+                   kdd_like(rng, 40, m, mean=300, values="normal"),
+                   kdd_like(rng, 20_000, m, powerlaw=True, values="normal")]).tocsr()
+    P = _staged(R2m, 16) if staged else Projector(R2m)
+    want = oracle_product(A, R2m)
+    assert_same_csr(P.matmul(A), *want)
+    Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
+    assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
