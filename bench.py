@@ -181,6 +181,9 @@ def main():
     if world > 1:
         dist.barrier()
     kernel_ms = e0.elapsed_time(e1) / args.steps
+    # workspace header (include/rp.h / rp_spgemm.hip Workspace): tiles taken, deferred tiles
+    hdr = ws[:24].cpu().numpy().view(np.uint32)
+    n_tiles_run, n_deferred = int(hdr[0]), int(hdr[4])
     t_max = t_wall
     if world > 1:
         tt = torch.tensor([t_wall], dtype=torch.float64, device=dev)
@@ -232,7 +235,10 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kernel_ms, "bytes_per_row": b_row,
                          "model": "B_row=(4+8a)+a(8+8r)+(4+8c)", "a": a, "r": rbar, "c": c,
-                         "traffic_source": "rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per launch, profiles/",
+                         "traffic_source": "rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per step, profiles/",
+                         "step_kernels": ["spgemm_lookback_kernel", "defer_copy_kernel"] +
+                                         (["stage_partition_kernel", "stage_gather_kernel"]
+                                          if args.staging == "on" else []),
                          "traffic_GBps": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
                          "random_line_ceiling_G_per_s": RANDOM_LINE_CEILING / 1e9,
                          "gathers_G_per_s": gathers_per_s / 1e9,
@@ -240,6 +246,7 @@ def main():
             "cpu_baseline": cpu,
             "r_setup_s": t_r,
             "r_broadcast_ms": t_bcast * 1e3,
+            "tiles": n_tiles_run, "deferred_tiles": n_deferred,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

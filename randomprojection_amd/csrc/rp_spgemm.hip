@@ -92,8 +92,13 @@ struct DeferSpace {
     unsigned char* slots;   // n_tiles x slot_bytes
     size_t slot_bytes;
 };
+// slot: row offsets (u16 x rpt+1) | columns (u16 x cap_p; p <= 32767) | values (T x cap_p)
 __host__ __device__ inline size_t defer_slot_bytes(int cap_p, int rpt, size_t vs) {
-    return ((2 * (size_t)(rpt + 1) + 15) & ~size_t(15)) + (((4 + vs) * (size_t)cap_p + 255) & ~size_t(255));
+    return ((2 * (size_t)(rpt + 1) + 15) & ~size_t(15)) + ((2 * (size_t)cap_p + 15) & ~size_t(15)) +
+           ((vs * (size_t)cap_p + 255) & ~size_t(255));
+}
+__host__ __device__ inline size_t defer_vals_offset(int cap_p, int rpt) {
+    return ((2 * (size_t)(rpt + 1) + 15) & ~size_t(15)) + ((2 * (size_t)cap_p + 15) & ~size_t(15));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -617,8 +622,8 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 T* __restrict__ Cxw = Cx;
                 if (deferred) {
                     const size_t hdr = (2 * (size_t)(caps.rpt + 1) + 15) & ~size_t(15);
-                    Cjw = reinterpret_cast<OI*>(slot + hdr);  // u32 columns (OI-typed view, see copy)
-                    Cxw = reinterpret_cast<T*>(slot + hdr + 4 * (size_t)caps.cap_p);
+                    Cjw = reinterpret_cast<OI*>(slot + hdr);  // u16 columns (OI-typed view, see copy)
+                    Cxw = reinterpret_cast<T*>(slot + defer_vals_offset(caps.cap_p, caps.rpt));
                     uint16_t* ro = reinterpret_cast<uint16_t*>(slot);
                     if (tid < nrows) ro[tid] = s_rank[s_rowS[tid]];
                     if (tid == 0) ro[nrows] = (uint16_t)tile_c;
@@ -642,7 +647,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                             pos += s_rank[re] - 1 - rk;  // reverse first-touch order
                         }
                         if (deferred) {
-                            reinterpret_cast<uint32_t*>(Cjw)[pos] = kr & 0xffffu;
+                            reinterpret_cast<uint16_t*>(Cjw)[pos] = (uint16_t)(kr & 0xffffu);
                             Cxw[pos] = s_pv[q];
                         } else {
                             Cj[G + pos] = (OI)(kr & 0xffffu);
@@ -873,8 +878,8 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
         const unsigned long long G = s_g;
         for (int r = tid; r < nrows; r += kBlock) Cp[row0 + r] = (OP)(G + ro[r]);
         if (G + cnt <= capacity) {
-            const uint32_t* cj = reinterpret_cast<const uint32_t*>(slot + hdr);
-            const T* cx = reinterpret_cast<const T*>(slot + hdr + 4 * (size_t)caps.cap_p);
+            const uint16_t* cj = reinterpret_cast<const uint16_t*>(slot + hdr);
+            const T* cx = reinterpret_cast<const T*>(slot + defer_vals_offset(caps.cap_p, caps.rpt));
             for (uint32_t q = tid; q < cnt; q += kBlock) {
                 Cj[G + q] = (OI)cj[q];
                 Cx[G + q] = cx[q];

@@ -12,7 +12,7 @@ run() { echo "== $*" >&2; "$@"; }
 run timeout -k 10 600 python -u bench.py $BA > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { tail -20 gpurun_out/bench_full.err; exit 4; }
 cat gpurun_out/bench_full.json
 run timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_${TAG}_trace -o trace -- python3 bench.py $PA > gpurun_out/prof_trace.log 2>&1 || { tail -20 gpurun_out/prof_trace.log; exit 5; }
-for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAVE_CYCLES"; do
+for pmc in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
   name=$(echo $pmc | tr ' ' '_')
   run timeout -s KILL 300 rocprofv3 --pmc $pmc -T --output-format csv -d gpurun_out/prof_${TAG}_pmc_$name -o pmc -- python3 bench.py $PA > gpurun_out/prof_pmc_$name.log 2>&1 || { tail -20 gpurun_out/prof_pmc_$name.log; exit 6; }
 done

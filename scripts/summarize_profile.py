@@ -1,14 +1,16 @@
 """Summarise a rocprofv3 session of bench.py (scripts/gpu_profile.sh) into profiles/.
 
-Reads gpurun_out/prof_<tag>_trace/*kernel_stats.csv and the separate PMC passes
+One projection step = the kernels of rp_project_device: spgemm_lookback_kernel (+ defer_copy_kernel,
++ stage_partition_kernel / stage_gather_kernel in staged mode). Reads
+gpurun_out/prof_<tag>_trace/*kernel_stats.csv and the separate PMC passes
 (gpurun_out/prof_<tag>_pmc_*/*counter_collection.csv) and writes
   profiles/<tag>_kernel_stats.csv      the rocprofv3 --stats summary (copied)
-  profiles/<tag>_summary.json          per-launch counters of the SpGEMM kernel + derived numbers
-  profiles/traffic_latest.json         HBM bytes per launch, read by bench.py (roofline.traffic)
+  profiles/<tag>_summary.json          per-step and per-kernel counters + derived numbers
+  profiles/traffic_latest.json         HBM bytes per step, read by bench.py (roofline.traffic)
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) counts 64 B per TCC_EA0_RDREQ while a
 request moves a 128-B line on gfx950 (the guide's "double it"), so read bytes = 2 x FETCH_SIZE x 1024;
-write bytes = WRITE_SIZE x 1024 (exact for these stores). The raw values are kept alongside.
+write bytes = WRITE_SIZE x 1024. The raw counter values are kept alongside.
 
     python scripts/summarize_profile.py --tag r01 --rows 119705032 --dist uniform
 """
@@ -21,16 +23,40 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "spgemm_lookback_kernel"
+STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel", "stage_partition_kernel", "stage_gather_kernel")
+
+
+def short(name):
+    for k in STEP_KERNELS:
+        if k in name:
+            return k
+    return None
 
 
 def pmc_means(path):
-    out = collections.defaultdict(list)
-    for f in glob.glob(os.path.join(path, "*counter_collection.csv")):
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"]:
-                out[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in out.items()}
+            k = short(r["Kernel_Name"])
+            if k:
+                out[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in out.items()}
+
+
+def derive(c, ms):
+    d = {}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        rd, wr = 2.0 * c["FETCH_SIZE"] * 1024, c["WRITE_SIZE"] * 1024
+        d.update(hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_bytes=rd + wr)
+        if ms:
+            d["hbm_GBps"] = (rd + wr) / (ms * 1e-3) / 1e9
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        d["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if "TCC_EA0_RDREQ_sum" in c:
+        d["read_requests"] = c["TCC_EA0_RDREQ_sum"]
+        if ms:
+            d["read_requests_G_per_s"] = c["TCC_EA0_RDREQ_sum"] / (ms * 1e-3) / 1e9
+    return d
 
 
 def main():
@@ -42,36 +68,32 @@ def main():
     args = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
+    summary = {"tag": args.tag, "rows": args.rows, "dist": args.dist, "kernels": {}}
     stats = glob.glob(os.path.join(args.src, f"prof_{args.tag}_trace", "*kernel_stats.csv"))
-    summary = {"tag": args.tag, "rows": args.rows, "dist": args.dist}
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{args.tag}_kernel_stats.csv"))
         for r in csv.DictReader(open(stats[0])):
-            if KERNEL in r["Name"]:
-                summary["kernel_avg_ms"] = float(r["AverageNs"]) / 1e6
-                summary["kernel_calls"] = int(r["Calls"])
-    counters = {}
+            k = short(r["Name"])
+            if k:
+                summary["kernels"][k] = {"avg_ms": float(r["AverageNs"]) / 1e6, "calls": int(r["Calls"])}
+    counters = collections.defaultdict(dict)
     for d in glob.glob(os.path.join(args.src, f"prof_{args.tag}_pmc_*")):
-        counters.update(pmc_means(d))
-    summary["counters_per_launch"] = counters
-    if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
-        rd = 2.0 * counters["FETCH_SIZE"] * 1024
-        wr = counters["WRITE_SIZE"] * 1024
-        summary["hbm_read_bytes"] = rd
-        summary["hbm_write_bytes"] = wr
-        summary["hbm_bytes_per_launch"] = rd + wr
-        if "kernel_avg_ms" in summary:
-            summary["hbm_GBps"] = (rd + wr) / (summary["kernel_avg_ms"] * 1e-3) / 1e9
-    if "TCC_HIT_sum" in counters and "TCC_MISS_sum" in counters:
-        h, m = counters["TCC_HIT_sum"], counters["TCC_MISS_sum"]
-        summary["l2_hit_rate"] = h / (h + m)
-    if "TCC_EA0_RDREQ_sum" in counters and "kernel_avg_ms" in summary:
-        summary["read_requests_per_launch"] = counters["TCC_EA0_RDREQ_sum"]
-        summary["read_requests_G_per_s"] = counters["TCC_EA0_RDREQ_sum"] / (summary["kernel_avg_ms"] * 1e-3) / 1e9
+        for k, cs in pmc_means(d).items():
+            counters[k].update(cs)
+    step_ms = sum(v["avg_ms"] for v in summary["kernels"].values()) or None
+    step_c = collections.Counter()
+    for k, cs in counters.items():
+        ent = summary["kernels"].setdefault(k, {})
+        ent["counters_per_launch"] = cs
+        ent.update(derive(cs, ent.get("avg_ms")))
+        step_c.update(cs)
+    summary["step_ms"] = step_ms
+    summary["step"] = derive(dict(step_c), step_ms)
     json.dump(summary, open(os.path.join(prof, f"{args.tag}_summary.json"), "w"), indent=1)
-    if "hbm_bytes_per_launch" in summary:
+    if "hbm_bytes" in summary["step"]:
         json.dump({"tag": args.tag, "rows": args.rows, "dist": args.dist,
-                   "hbm_bytes_per_launch": summary["hbm_bytes_per_launch"],
+                   "hbm_bytes_per_launch": summary["step"]["hbm_bytes"],
+                   "note": "per projection step (all kernels of rp_project_device)",
                    "source": f"profiles/{args.tag}_summary.json"},
                   open(os.path.join(prof, "traffic_latest.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
