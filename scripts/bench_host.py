@@ -40,11 +40,11 @@ def main():
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--part-rows", type=int, default=100_000)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--libsvm-rows", type=int, default=1_000_000)
     args = ap.parse_args()
 
     import torch  # noqa: F401  (one HIP runtime; see _native.load)
 
-    from oracle import smmp
     from randomprojection_amd import Projector, random_project_mappartitions_function, srp_matrix as sm
     from randomprojection_amd.linalg import SparseVector
 
@@ -69,17 +69,59 @@ def main():
     out = list(random_project_mappartitions_function(iter(rows), R))
     dropin_s = time.perf_counter() - t0
     assert len(out) == len(rows)
+    # the reference's own recipe restated with the same scipy calls (oracle/recipe.py), 1 core,
+    # on the same rows and the recipe's CSC operand (components_.T)
+    from oracle.recipe import recipe_partition
+
     n_ref = min(args.part_rows, 20_000)
+    Rcsc = R.tocsc()
+    recipe_partition(rows[:100], Rcsc)
     t0 = time.perf_counter()
-    smmp.partition_function_py(rows[:n_ref], R)
+    ref_out = recipe_partition(rows[:n_ref], Rcsc)
     ref_s = (time.perf_counter() - t0) * args.part_rows / n_ref
+    for a, b in zip(ref_out[:200], out[:200]):  # same answer, checked on a prefix
+        assert a[0] == b[0] and np.array_equal(a[2].indices, b[2].indices)
+        assert np.array_equal(a[2].values, b[2].values)
+    # boundary 3: libsvm text file -> GPU parse -> GPU projection -> host CSR (libsvm.project_libsvm)
+    import tempfile
+
+    from randomprojection_amd import libsvm
+
+    n_txt = min(args.rows, args.libsvm_rows)
+    T = A[:n_txt]
+    lines = []
+    for i in range(n_txt):
+        s_, e_ = T.indptr[i], T.indptr[i + 1]
+        lines.append(("1" if i & 1 else "0") + "".join(f" {j + 1}:1" for j in T.indices[s_:e_]))
+    text = ("\n".join(lines) + "\n").encode()
+    with tempfile.NamedTemporaryFile(suffix=".libsvm", delete=False) as fh:
+        fh.write(text)
+        path = fh.name
+    try:
+        list(libsvm.project_libsvm(path, P, chunk_bytes=1 << 20))  # warm
+        t0 = time.perf_counter()
+        got = 0
+        for _ids, _labels, Cc in libsvm.project_libsvm(path, P, chunk_bytes=64 << 20):
+            got += Cc.shape[0]
+        txt_s = time.perf_counter() - t0
+        assert got == n_txt
+    finally:
+        os.unlink(path)
+
     print(json.dumps({
         "boundary": "host CSR in -> host CSR out (PCIe-inclusive)",
         "rows": args.rows, "host_rows_per_s": host_rows_s, "nnz_out": int(C.nnz),
         "dropin_partition": {"rows": args.part_rows, "rows_per_s": args.part_rows / dropin_s,
                              "us_per_row": dropin_s / args.part_rows * 1e6},
         "recipe_restatement_1core": {"rows_per_s": args.part_rows / ref_s, "us_per_row": ref_s / args.part_rows * 1e6,
-                                     "note": "oracle.smmp.partition_function_py: row dicts -> CSR -> C scipy-kernel restatement -> sorted f64 rows, 1 core"},
+                                     "rows_timed": n_ref,
+                                     "note": "oracle/recipe.py: the reference partition function's own scipy calls "
+                                             "(per-row coo->csr, vstack, CSR@CSC dot, per-row Vectors.sparse), 1 core"},
+        "dropin_speedup_vs_recipe": (ref_s / args.part_rows) / (dropin_s / args.part_rows),
+        "libsvm_text_to_host_csr": {"rows": n_txt, "text_bytes": len(text), "rows_per_s": n_txt / txt_s,
+                                    "text_GB_per_s": len(text) / txt_s / 1e9,
+                                    "note": "boundary 3: file (page cache) -> 64 MB chunks -> GPU parse + "
+                                            "projection -> host CSR, sorted rows"},
     }))
 
 

@@ -67,3 +67,25 @@ def test_threaded_driver_counts(golden):
     R = golden_R(golden, 1).tocsr()
     total = smmp.project_mt(A.indptr, A.indices, A.data, R.indptr, R.indices, R.data, R.shape[1], 4)
     assert total == golden["C_kdd_ones_indptr"][-1]
+
+
+def test_recipe_restatement_matches_kernel_restatement():
+    """oracle/recipe.py (the reference's scipy call sequence) == oracle.smmp's partition restatement."""
+    from oracle.recipe import recipe_partition
+    from randomprojection_amd import srp_matrix as sm
+    from randomprojection_amd.linalg import SparseVector
+
+    m = 20_000
+    R = sm.projection_operand(sm.sparse_random_matrix(256, m, random_state=123))
+    rng = np.random.default_rng(4)
+    rows = []
+    for i in range(300):
+        c = np.unique(rng.integers(0, m, 1 + rng.poisson(10)))
+        rows.append({"id": 10 * i, "label": float(i % 2),
+                     "features": SparseVector(m, c.astype(np.int32), rng.standard_normal(c.size))})
+    a = recipe_partition(rows, R.tocsc())
+    b = smmp.partition_function_py(rows, R)
+    assert len(a) == len(b) == 300
+    for (i1, l1, v), (i2, l2, jj, xx) in zip(a, b):
+        assert i1 == i2 and l1 == l2
+        assert np.array_equal(v.indices, jj) and np.array_equal(v.values.view(np.uint64), xx.view(np.uint64))
