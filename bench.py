@@ -143,8 +143,12 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     if args.staging != "auto" or args.stage_shift:
         P.set_staging(args.staging, args.stage_shift)
-    ws = torch.empty(P.workspace_bytes(args.rows, nnz_a), dtype=torch.uint8, device=dev)
-    cap = int(1.3 * nnz_a * P.nnz / P.m) + 1024
+    try:  # full workspace (deferred tile output + staging); the minimal one if HBM is short
+        ws = torch.empty(P.workspace_bytes(args.rows, nnz_a), dtype=torch.uint8, device=dev)
+    except torch.OutOfMemoryError:
+        log(f"[rank {rank}] full workspace does not fit: blocking look-back only")
+        ws = torch.empty(P.workspace_bytes(args.rows), dtype=torch.uint8, device=dev)
+    cap = int(1.05 * nnz_a * P.nnz / P.m) + 65536
     Cj = torch.empty(cap, dtype=torch.int32, device=dev)
     Cx = torch.empty(cap, dtype=torch.float32, device=dev)
     ip_dtype = torch.int32 if cap < 2**31 else torch.int64

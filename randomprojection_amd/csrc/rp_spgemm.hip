@@ -76,30 +76,27 @@ struct Workspace {              // device memory header; tile states follow at +
     unsigned int tile_counter;
     unsigned int error;
     unsigned long long total;
-    unsigned int n_deferred;    // tiles that parked their output in a temp slot (see defer below)
+    unsigned int n_deferred;    // tiles that parked their output in the pool (see defer below)
     unsigned int pad0;
-    unsigned long long pad[5];
+    unsigned long long pool_used;  // entries of the deferred-output pool handed out
+    unsigned long long pad[4];
 };
 
-// Deferred output (DESIGN.md §3c): a tile whose exclusive prefix is not published within
-// `defer_polls` look-back polls does not wait: it parks its finished output in its temp slot
-// (row offsets + entries in final order), leaves its aggregate published, appends itself to the
-// deferred list and exits; defer_copy_kernel later resolves its prefix (every state is final
-// then) and copies the slot to its place. Waiting tiles hold LDS and waves idle: measured 7.6 ms
-// of 32.9 on configs[1] (direct gathers).
+// Deferred output (DESIGN.md §3a): a tile whose exclusive prefix is not published within
+// `defer_polls` look-back polls does not wait: it takes exactly its entry count from a shared
+// pool (one atomic), parks its finished output there (columns u16, values T, in final order) and
+// its row offsets in its header, leaves its aggregate published, appends itself to the deferred
+// list and exits; defer_copy_kernel later resolves its prefix (every state is final then) and
+// copies the entries to their place. A tile that finds the pool exhausted waits instead. Waiting
+// tiles hold LDS and waves idle: measured 7.6 ms of 32.9 on configs[1] (direct gathers).
 struct DeferSpace {
-    unsigned int* list;     // n_tiles
-    unsigned char* slots;   // n_tiles x slot_bytes
-    size_t slot_bytes;
+    unsigned int* list;          // n_tiles
+    unsigned long long* pofs;    // n_tiles: pool offset of a deferred tile
+    uint16_t* hdr;               // n_tiles x (rpt + 1): row offsets, [rows] = count
+    uint16_t* cols;              // pool_cap
+    unsigned char* vals;         // pool_cap x sizeof(T)
+    unsigned long long pool_cap;
 };
-// slot: row offsets (u16 x rpt+1) | columns (u16 x cap_p; p <= 32767) | values (T x cap_p)
-__host__ __device__ inline size_t defer_slot_bytes(int cap_p, int rpt, size_t vs) {
-    return ((2 * (size_t)(rpt + 1) + 15) & ~size_t(15)) + ((2 * (size_t)cap_p + 15) & ~size_t(15)) +
-           ((vs * (size_t)cap_p + 255) & ~size_t(255));
-}
-__host__ __device__ inline size_t defer_vals_offset(int cap_p, int rpt) {
-    return ((2 * (size_t)(rpt + 1) + 15) & ~size_t(15)) + ((2 * (size_t)cap_p + 15) & ~size_t(15));
-}
 
 // ------------------------------------------------------------------------------------------
 // R layouts
@@ -466,6 +463,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     __shared__ unsigned int s_tile;
     __shared__ int s_heavy;
     __shared__ unsigned long long s_off;
+    __shared__ unsigned long long s_pool;
 
     unsigned long long* states = reinterpret_cast<unsigned long long*>(ws + 1);
     const int tid = threadIdx.x;
@@ -613,24 +611,37 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 }
                 __syncthreads();
                 STAMP(5);
+                if (s_off == ~0ull) {  // uniform: no prefix yet -> take pool space, or wait
+                    if (tid == 0) {
+                        const unsigned long long o = atomicAdd(&ws->pool_used, (unsigned long long)tile_c);
+                        s_pool = o + tile_c <= dfr.pool_cap ? o : ~0ull;
+                        if (s_pool != ~0ull) {
+                            dfr.pofs[tile] = o;
+                            dfr.list[atomicAdd(&ws->n_deferred, 1u)] = tile;
+                        }
+                    }
+                    __syncthreads();
+                    if (s_pool == ~0ull) {
+                        if (tid < 64) {
+                            const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, false);
+                            if (tid == 0) s_off = g;
+                        }
+                        __syncthreads();
+                    }
+                }
                 const bool deferred = s_off == ~0ull;  // uniform
                 const unsigned long long G = deferred ? 0ull : s_off;
-                // deferred: entries go to the tile's temp slot at their tile-local positions and the
-                // row offsets to the slot header; defer_copy_kernel adds the prefix later
-                unsigned char* slot = dfr.slots + (size_t)tile * dfr.slot_bytes;
-                OI* __restrict__ Cjw = Cj;
-                T* __restrict__ Cxw = Cx;
+                // deferred: entries go to the pool at their tile-local positions and the row offsets
+                // to the tile's header; defer_copy_kernel adds the prefix later
                 if (deferred) {
-                    const size_t hdr = (2 * (size_t)(caps.rpt + 1) + 15) & ~size_t(15);
-                    Cjw = reinterpret_cast<OI*>(slot + hdr);  // u16 columns (OI-typed view, see copy)
-                    Cxw = reinterpret_cast<T*>(slot + defer_vals_offset(caps.cap_p, caps.rpt));
-                    uint16_t* ro = reinterpret_cast<uint16_t*>(slot);
+                    uint16_t* ro = dfr.hdr + (size_t)tile * (caps.rpt + 1);
                     if (tid < nrows) ro[tid] = s_rank[s_rowS[tid]];
                     if (tid == 0) ro[nrows] = (uint16_t)tile_c;
-                    if (tid == 0) dfr.list[atomicAdd(&ws->n_deferred, 1u)] = tile;
                 } else if (tid < nrows) {
                     Cp[row0 + tid] = (OP)(G + s_rank[s_rowS[tid]]);
                 }
+                uint16_t* __restrict__ pc = dfr.cols + (deferred ? s_pool : 0ull);
+                T* __restrict__ pv = reinterpret_cast<T*>(dfr.vals) + (deferred ? s_pool : 0ull);
                 if ((deferred || G + tile_c <= capacity) && RP_EXP != 4) {
                     // kept leaders write straight into the tile's contiguous output range
                     for (uint32_t q = tid; q < P_t; q += kBlock) {
@@ -647,8 +658,8 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                             pos += s_rank[re] - 1 - rk;  // reverse first-touch order
                         }
                         if (deferred) {
-                            reinterpret_cast<uint16_t*>(Cjw)[pos] = (uint16_t)(kr & 0xffffu);
-                            Cxw[pos] = s_pv[q];
+                            pc[pos] = (uint16_t)(kr & 0xffffu);
+                            pv[pos] = s_pv[q];
                         } else {
                             Cj[G + pos] = (OI)(kr & 0xffffu);
                             Cx[G + pos] = s_pv[q];
@@ -862,14 +873,14 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
     unsigned long long* states = reinterpret_cast<unsigned long long*>(ws + 1);
     const unsigned nd = ws->n_deferred;
     const int tid = threadIdx.x;
-    const size_t hdr = (2 * (size_t)(caps.rpt + 1) + 15) & ~size_t(15);
+    const T* vals = reinterpret_cast<const T*>(dfr.vals);
     for (unsigned i = blockIdx.x; i < nd; i += gridDim.x) {
         const unsigned tile = dfr.list[i];
-        const unsigned char* slot = dfr.slots + (size_t)tile * dfr.slot_bytes;
-        const uint16_t* ro = reinterpret_cast<const uint16_t*>(slot);
+        const uint16_t* ro = dfr.hdr + (size_t)tile * (caps.rpt + 1);
         const int64_t row0 = (int64_t)tile * caps.rpt;
         const int nrows = (int)std::min<int64_t>(caps.rpt, n_rows - row0);
         const uint32_t cnt = ro[nrows];
+        const unsigned long long po = dfr.pofs[tile];
         if (tid < 64) {
             const unsigned long long g = lookback_wave(states, tile, cnt, ws, -1, false);
             if (tid == 0) s_g = g;
@@ -877,14 +888,11 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
         __syncthreads();
         const unsigned long long G = s_g;
         for (int r = tid; r < nrows; r += kBlock) Cp[row0 + r] = (OP)(G + ro[r]);
-        if (G + cnt <= capacity) {
-            const uint16_t* cj = reinterpret_cast<const uint16_t*>(slot + hdr);
-            const T* cx = reinterpret_cast<const T*>(slot + defer_vals_offset(caps.cap_p, caps.rpt));
+        if (G + cnt <= capacity)
             for (uint32_t q = tid; q < cnt; q += kBlock) {
-                Cj[G + q] = (OI)cj[q];
-                Cx[G + q] = cx[q];
+                Cj[G + q] = (OI)dfr.cols[po + q];
+                Cx[G + q] = vals[po + q];
             }
-        }
         if (tile == n_tiles - 1 && tid == 0) {
             Cp[n_rows] = (OP)(G + cnt);
             ws->total = G + cnt;
@@ -1096,7 +1104,9 @@ struct Plan {
     bool defer = false;
     int sb = 0, nb = 0;
     uint32_t ostride = 0;
-    size_t head = 0, dlist = 0, slots = 0, slot_bytes = 0, te = 0, offt = 0, s = 0, d = 0, sx = 0;
+    size_t head = 0, dlist = 0, pofs = 0, dhdr = 0, pcols = 0, pvals = 0, te = 0, offt = 0, s = 0,
+           d = 0, sx = 0;
+    unsigned long long pool_cap = 0;
     size_t total = 0;
 };
 
@@ -1114,12 +1124,16 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
     auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
     pl.head = al(sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(pl.n_tiles, 1));
     pl.total = pl.head;
-    if (pl.n_tiles > 0 && allow_defer) {  // deferred-output list and temp slots
+    if (pl.n_tiles > 0 && allow_defer && nnz_a >= 0) {  // deferred-output list, headers, pool
         pl.defer = true;
+        // pool: the expected products (>= outputs) + 2% + 64K entries; a tile finding it full waits
+        pl.pool_cap = (unsigned long long)(1.02 * ppe * (double)nnz_a) + 65536ull;
         pl.dlist = pl.total;
-        pl.slot_bytes = defer_slot_bytes(pl.caps.cap_p, pl.caps.rpt, (size_t)vs);
-        pl.slots = pl.dlist + al(4 * (size_t)pl.n_tiles);
-        pl.total = pl.slots + pl.slot_bytes * (size_t)pl.n_tiles;
+        pl.pofs = pl.dlist + al(4 * (size_t)pl.n_tiles);
+        pl.dhdr = pl.pofs + al(8 * (size_t)pl.n_tiles);
+        pl.pcols = pl.dhdr + al(2 * (size_t)(pl.caps.rpt + 1) * (size_t)pl.n_tiles);
+        pl.pvals = pl.pcols + al(2 * (size_t)pl.pool_cap);
+        pl.total = pl.pvals + al((size_t)vs * (size_t)pl.pool_cap);
     }
     const bool can = h->layout == RP_LAYOUT_PACKED && h->W32.p && nnz_a > 0 && pl.n_tiles > 0;
     const bool want = h->stage_mode == 1 ||
@@ -1143,9 +1157,12 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
     return pl;
 }
 
-int defer_polls_setting() {
+// Polls before a tile defers. Measured optimum differs with the tile shape: 2 on configs[1]
+// (256-row tiles whose random-gather latency varies widely: 27.7 ms vs 32.7 waiting), 8 on
+// configs[3] (29-row tiles of 100-nnz rows hitting L2: 268 ms vs 285 waiting, 325 at 2 polls).
+int defer_polls_setting(const Caps& caps) {
     const char* e = getenv("RP_DEFER_POLLS");  // tests and tuning: -1 never defer, 0 defer at once
-    return e ? atoi(e) : kDeferPolls;
+    return e ? atoi(e) : (caps.rpt >= 128 ? kDeferPolls : 4 * kDeferPolls);
 }
 
 template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED>
@@ -1156,12 +1173,14 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     char* base = reinterpret_cast<char*>(ws);
     DeferSpace dfr{reinterpret_cast<unsigned int*>(base + pl.dlist),
-                   reinterpret_cast<unsigned char*>(base + pl.slots), pl.slot_bytes};
+                   reinterpret_cast<unsigned long long*>(base + pl.pofs),
+                   reinterpret_cast<uint16_t*>(base + pl.dhdr), reinterpret_cast<uint16_t*>(base + pl.pcols),
+                   reinterpret_cast<unsigned char*>(base + pl.pvals), pl.pool_cap};
     hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED>), dim3(n_tiles), dim3(kBlock), lds, st,
                        R, mag, (int)h->p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
                        (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order,
-                       ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting() : -1);
+                       ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting(pl.caps) : -1);
     HIP_TRY(hipGetLastError());
     if (pl.defer) {
         hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, 4096u)), dim3(kBlock), 0,
