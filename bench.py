@@ -88,10 +88,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N>1 path on a one-GPU box only: every rank on cuda:0 over gloo
+    # (RCCL refuses two ranks on one device); the driver's multi-GPU runs use neither
+    rehearse = os.environ.get("RP_BENCH_REHEARSE_ONE_GPU") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     # ---- R: generated once on rank 0 (sklearn-identical), packed and uploaded, broadcast over RCCL
     t0 = time.perf_counter()
