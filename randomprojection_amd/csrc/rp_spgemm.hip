@@ -910,6 +910,16 @@ __global__ void convert_kernel(const S* __restrict__ s, D* __restrict__ d, int64
         d[i] = (D)s[i];
 }
 
+// first position (atomicMin) of a column index outside [0, m): host-path input validation
+__global__ void check_columns_kernel(const int32_t* __restrict__ Aj, int64_t n, int64_t m,
+                                     unsigned long long* first_bad) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t j = Aj[i];
+        if (j < 0 || (int64_t)j >= m) atomicMin(first_bad, (unsigned long long)i);
+    }
+}
+
 template <typename S, typename D>
 __global__ void rebase_kernel(const S* __restrict__ s, D* __restrict__ d, int64_t n, int64_t add) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -1056,7 +1066,7 @@ struct rp_projector {
     // generic
     DevBuf Bp, Bj, Bx32, Bx64;
     // internal workspace and host-path staging
-    DevBuf ws;
+    DevBuf ws, ws_check;
     DevBuf a_ptr, a_idx, a_val;
     std::mutex mu;
 };
@@ -1721,11 +1731,11 @@ int rp_project_host_begin(rp_projector* h, const rp_csr_in* a, int32_t order, rp
     const int64_t b0 = ptr_at(a->indptr, a->indptr_type, 0);
     const int64_t nnz_a = ptr_at(a->indptr, a->indptr_type, n) - b0;
     if (nnz_a < 0) return fail(RP_ERR_INVALID, "A indptr decreasing");
-    for (int64_t q = 0; q < nnz_a; ++q) {
-        const int32_t j = a->indices[b0 + q];
-        if (j < 0 || j >= h->m)
-            return fail(RP_ERR_INVALID, "A column index %d out of range [0, %lld)", j, (long long)h->m);
-    }
+    // the kernels index A through indptr: it must be monotone (O(n) here); the column indices are
+    // checked on the device after the upload (O(nnz) there, not on the host)
+    for (int64_t i = 0; i < n; ++i)
+        if (ptr_at(a->indptr, a->indptr_type, i + 1) < ptr_at(a->indptr, a->indptr_type, i))
+            return fail(RP_ERR_INVALID, "A indptr decreasing at row %lld", (long long)i);
     std::lock_guard<std::mutex> lock(h->mu);
     HIP_TRY(hipSetDevice(h->device));
     rp_result* r = new (std::nothrow) rp_result();
@@ -1741,9 +1751,24 @@ int rp_project_host_begin(rp_projector* h, const rp_csr_in* a, int32_t order, rp
         delete r;
         return rc;
     }
-    std::vector<int64_t> ptr64((size_t)n + 1);
-    for (int64_t i = 0; i <= n; ++i) ptr64[(size_t)i] = ptr_at(a->indptr, a->indptr_type, i) - b0;
-    hipError_t e = hipMemcpy(h->a_ptr.p, ptr64.data(), 8 * (size_t)(n + 1), hipMemcpyHostToDevice);
+    // indptr goes up as given (into the tail of a_ptr when int32) and is rebased to int64 on the device
+    const size_t grid = (size_t)std::min<int64_t>(std::max<int64_t>((n + 256) / 256, 1), 65536);
+    hipError_t e;
+    if (a->indptr_type == RP_I64) {
+        e = hipMemcpy(h->a_ptr.p, a->indptr, 8 * (size_t)(n + 1), hipMemcpyHostToDevice);
+        if (e == hipSuccess && b0 != 0)
+            hipLaunchKernelGGL((rebase_kernel<int64_t, int64_t>), dim3((unsigned)grid), dim3(256), 0, nullptr,
+                               (const int64_t*)h->a_ptr.p, (int64_t*)h->a_ptr.p, n + 1, -b0);
+    } else {
+        if ((rc = r->cp.ensure(4 * (size_t)(n + 1), h->device))) {  // scratch for the int32 copy
+            delete r;
+            return rc;
+        }
+        e = hipMemcpy(r->cp.p, a->indptr, 4 * (size_t)(n + 1), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            hipLaunchKernelGGL((rebase_kernel<int32_t, int64_t>), dim3((unsigned)grid), dim3(256), 0, nullptr,
+                               (const int32_t*)r->cp.p, (int64_t*)h->a_ptr.p, n + 1, -b0);
+    }
     if (e == hipSuccess && nnz_a > 0)
         e = hipMemcpy(h->a_idx.p, a->indices + b0, 4 * (size_t)nnz_a, hipMemcpyHostToDevice);
     if (e == hipSuccess && nnz_a > 0)
@@ -1752,6 +1777,24 @@ int rp_project_host_begin(rp_projector* h, const rp_csr_in* a, int32_t order, rp
     if (e != hipSuccess) {
         delete r;
         return fail(RP_ERR_HIP, "A upload: %s", hipGetErrorString(e));
+    }
+    if (nnz_a > 0) {
+        if ((rc = h->ws_check.ensure(8, h->device))) {
+            delete r;
+            return rc;
+        }
+        const unsigned long long none = ~0ull;
+        HIP_TRY(hipMemcpy(h->ws_check.p, &none, 8, hipMemcpyHostToDevice));
+        const unsigned cg = (unsigned)std::min<int64_t>((nnz_a + 255) / 256, 16384);
+        hipLaunchKernelGGL(check_columns_kernel, dim3(cg), dim3(256), 0, nullptr, (const int32_t*)h->a_idx.p,
+                           nnz_a, h->m, (unsigned long long*)h->ws_check.p);
+        unsigned long long bad = 0;
+        HIP_TRY(hipMemcpy(&bad, h->ws_check.p, 8, hipMemcpyDeviceToHost));
+        if (bad != ~0ull) {
+            const int32_t j = a->indices[b0 + (int64_t)bad];
+            delete r;
+            return fail(RP_ERR_INVALID, "A column index %d out of range [0, %lld)", j, (long long)h->m);
+        }
     }
     rp_csr_in ad{n, h->a_ptr.p, RP_I64, (const int32_t*)h->a_idx.p, h->a_val.p, a->data_type, nnz_a};
     // capacity guess from the expected products, exact retry on overflow
@@ -1791,22 +1834,31 @@ int rp_result_fetch(rp_result* r, void* indptr, int32_t indptr_type, void* indic
     if (r->nnz > 0 && (!indices || !data)) return fail(RP_ERR_INVALID, "NULL output arrays");
     HIP_TRY(hipSetDevice(r->h->device));
     const int64_t n = r->n_rows;
+    // type conversions run on the device (into a scratch buffer), then one copy each
+    DevBuf conv;
+    const size_t cbytes = std::max<size_t>(indptr_type == RP_I32 ? 4 * (size_t)(n + 1) : 0,
+                                           indices_type == RP_I64 ? 8 * (size_t)r->nnz : 0);
+    if (cbytes) {
+        int rc = conv.ensure(cbytes, r->h->device);
+        if (rc) return rc;
+    }
+    auto grid_for = [](int64_t k) { return dim3((unsigned)std::min<int64_t>(std::max<int64_t>((k + 255) / 256, 1), 65536)); };
     if (indptr_type == RP_I64) {
         HIP_TRY(hipMemcpy(indptr, r->cp.p, 8 * (size_t)(n + 1), hipMemcpyDeviceToHost));
     } else {
-        std::vector<int64_t> tmp((size_t)n + 1);
-        HIP_TRY(hipMemcpy(tmp.data(), r->cp.p, 8 * (size_t)(n + 1), hipMemcpyDeviceToHost));
-        int32_t* o = (int32_t*)indptr;
-        for (int64_t i = 0; i <= n; ++i) o[i] = (int32_t)tmp[(size_t)i];
+        hipLaunchKernelGGL((convert_kernel<int64_t, int32_t>), grid_for(n + 1), dim3(256), 0, nullptr,
+                           (const int64_t*)r->cp.p, (int32_t*)conv.p, n + 1);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpy(indptr, conv.p, 4 * (size_t)(n + 1), hipMemcpyDeviceToHost));
     }
     if (r->nnz > 0) {
         if (indices_type == RP_I32) {
             HIP_TRY(hipMemcpy(indices, r->cj.p, 4 * (size_t)r->nnz, hipMemcpyDeviceToHost));
         } else {
-            std::vector<int32_t> tmp((size_t)r->nnz);
-            HIP_TRY(hipMemcpy(tmp.data(), r->cj.p, 4 * (size_t)r->nnz, hipMemcpyDeviceToHost));
-            int64_t* o = (int64_t*)indices;
-            for (int64_t i = 0; i < r->nnz; ++i) o[i] = tmp[(size_t)i];
+            hipLaunchKernelGGL((convert_kernel<int32_t, int64_t>), grid_for(r->nnz), dim3(256), 0, nullptr,
+                               (const int32_t*)r->cj.p, (int64_t*)conv.p, r->nnz);
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipMemcpy(indices, conv.p, 8 * (size_t)r->nnz, hipMemcpyDeviceToHost));
         }
         HIP_TRY(hipMemcpy(data, r->cx.p, (size_t)dtype_size(r->value_type) * (size_t)r->nnz,
                           hipMemcpyDeviceToHost));

@@ -68,13 +68,19 @@ def parse_device(text, n_bytes: int, num_features: int, device: int = 0, stream:
 
 
 def _to_device(buf, device):
+    """Copy a bytes-like chunk (bytes, bytearray, or a memoryview of the mapped file) to a 16-byte
+    aligned device buffer with one host->device copy and no host-side copy."""
+    import warnings
+
     import torch
 
     n = len(buf)
     t = torch.empty((n + 15) // 16 * 16 + 16, dtype=torch.uint8, device=torch.device("cuda", device))
     if n:
-        t[:n].copy_(torch.frombuffer(bytearray(buf) if not isinstance(buf, (bytearray, memoryview)) else buf,
-                                     dtype=torch.uint8))
+        with warnings.catch_warnings():  # read-only source (mapped file): torch only reads it
+            warnings.simplefilter("ignore", UserWarning)
+            src = torch.from_numpy(np.frombuffer(buf, dtype=np.uint8, count=n))
+        t[:n].copy_(src)
     return t, n
 
 
@@ -87,8 +93,10 @@ def parse_bytes(buf, num_features: int, device: int = 0):
     return labels.cpu().numpy(), X
 
 
-def iter_chunks(path: str, chunk_bytes: int = DEFAULT_CHUNK):
-    """Newline-aligned chunks of a file (memory-mapped, never loaded whole)."""
+def iter_chunks(path: str, chunk_bytes: int = DEFAULT_CHUNK, copy: bool = True):
+    """Newline-aligned chunks of a file (memory-mapped, never loaded whole). ``copy=False`` yields
+    memoryviews of the mapping instead of bytes: each is valid until the next chunk is requested
+    and must be released (``del``) by then."""
     size = os.path.getsize(path)
     if size == 0:
         return
@@ -103,7 +111,14 @@ def iter_chunks(path: str, chunk_bytes: int = DEFAULT_CHUNK):
                 else:  # one line longer than a chunk: extend to its end
                     nxt = mm.find(b"\n", end)
                     end = size if nxt < 0 else nxt + 1
-            yield memoryview(mm)[start:end].tobytes()
+            view = memoryview(mm)[start:end]
+            if copy:
+                chunk = view.tobytes()
+                view.release()
+                yield chunk
+            else:
+                yield view
+                view.release()
             start = end
 
 
@@ -120,8 +135,9 @@ def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order
     import torch
 
     dev = projector.device
-    for ci, buf in enumerate(iter_chunks(path, chunk_bytes)):
+    for ci, buf in enumerate(iter_chunks(path, chunk_bytes, copy=False)):
         t, n = _to_device(buf, dev)
+        del buf  # the view must be gone before the next chunk (the mapping closes at the end)
         labels, Ap, Aj, Ax = parse_device(t, n, projector.m, dev)
         del t
         rows = int(labels.numel())
