@@ -588,13 +588,30 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     const uint32_t kr = s_pkr[q];
                     const uint32_t r = kr >> 16;
                     const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
+                    // keys are read four at a time (one ds_read_b128 from a 16-byte aligned group,
+                    // out-of-range lanes masked): a quarter of the dependent LDS round trips
+                    const uint4* pk4 = reinterpret_cast<const uint4*>(s_pkr);
                     bool leader = true;
-                    for (uint32_t u = rs; u < q; ++u) leader &= s_pkr[u] != kr;
+                    for (uint32_t g = rs >> 2; g <= (q - 1) >> 2 && q > rs; ++g) {
+                        const uint4 k4 = pk4[g];
+                        const uint32_t b = g << 2;
+                        leader &= !((k4.x == kr) & (b >= rs) & (b < q));
+                        leader &= !((k4.y == kr) & (b + 1 >= rs) & (b + 1 < q));
+                        leader &= !((k4.z == kr) & (b + 2 >= rs) & (b + 2 < q));
+                        leader &= !((k4.w == kr) & (b + 3 >= rs) & (b + 3 < q));
+                    }
                     uint16_t flag = 0;
                     if (leader) {
                         T sum = tadd<T>(T(0), s_pv[q]);
-                        for (uint32_t u = q + 1; u < re; ++u)
-                            if (s_pkr[u] == kr) sum = tadd<T>(sum, s_pv[u]);
+                        for (uint32_t g = (q + 1) >> 2; (g << 2) < re; ++g) {
+                            const uint4 k4 = pk4[g];
+                            const uint32_t b = g << 2;
+                            // in sequence order; only matching products (same row and column) add
+                            if (k4.x == kr && b > q && b < re) sum = tadd<T>(sum, s_pv[b]);
+                            if (k4.y == kr && b + 1 > q && b + 1 < re) sum = tadd<T>(sum, s_pv[b + 1]);
+                            if (k4.z == kr && b + 2 > q && b + 2 < re) sum = tadd<T>(sum, s_pv[b + 2]);
+                            if (k4.w == kr && b + 3 > q && b + 3 < re) sum = tadd<T>(sum, s_pv[b + 3]);
+                        }
                         s_pv[q] = sum;  // position q is read by no other leader (column differs)
                         flag = sum != T(0) ? 1 : 0;
                     }
@@ -1120,6 +1137,7 @@ struct Plan {
     size_t total = 0;
 };
 
+constexpr unsigned kDeferCopyGrid = 32768;  // copy workgroups (grid-stride over the deferred list)
 constexpr int kDeferPolls = 2;                 // look-back polls before a tile defers its output
 constexpr bool kStageAuto = false;              // auto picks staging (off until it measures faster)
 constexpr int64_t kStageMinNnz = 1 << 22;      // auto: stage only launches this large
@@ -1193,7 +1211,7 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
                        ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting(pl.caps) : -1);
     HIP_TRY(hipGetLastError());
     if (pl.defer) {
-        hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, 4096u)), dim3(kBlock), 0,
+        hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, kDeferCopyGrid)), dim3(kBlock), 0,
                            st, dfr, ws, pl.caps, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices,
                            (T*)c->data, (unsigned long long)c->capacity);
         HIP_TRY(hipGetLastError());

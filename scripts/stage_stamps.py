@@ -21,6 +21,10 @@ def main():
     ap.add_argument("--rows", type=int, default=20_000_000)
     ap.add_argument("--dist", default="uniform")
     ap.add_argument("--staging", choices=["auto", "on", "off"], default="auto")
+    ap.add_argument("--m", type=int, default=None)
+    ap.add_argument("--p", type=int, default=4096)
+    ap.add_argument("--mean-extra", type=float, default=10.0)
+    ap.add_argument("--rpt", type=int, default=256, help="rows per tile the launch will use")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stamps.json"))
     args = ap.parse_args()
 
@@ -32,11 +36,12 @@ def main():
     lib.rp_debug_stamps.argtypes = [ctypes.c_void_p]
     from randomprojection_amd import Projector, srp_matrix as sm, synth
 
-    R = sm.projection_operand(sm.sparse_random_matrix(4096, sm.KDD_M, random_state=123))
+    m = args.m or sm.KDD_M
+    R = sm.projection_operand(sm.sparse_random_matrix(args.p, m, random_state=123))
     P = Projector(R)
     P.set_staging(args.staging)
-    Ap, Aj, Ax = synth.kdd_rows_device(args.rows, sm.KDD_M, seed=7, dist=args.dist)
-    n_tiles = (args.rows + 255) // 256
+    Ap, Aj, Ax = synth.kdd_rows_device(args.rows, m, seed=7, dist=args.dist, mean_extra=args.mean_extra)
+    n_tiles = (args.rows + args.rpt - 1) // args.rpt
     stamps = torch.zeros(n_tiles * 8, dtype=torch.int64, device="cuda")
     cap = int(1.3 * Aj.numel() * P.nnz / P.m) + 1024
     Cp = torch.empty(args.rows + 1, dtype=torch.int32, device="cuda")
