@@ -282,9 +282,20 @@ def cpu_baseline(args, Ap, Aj, Ax, R_host):
     t0 = time.perf_counter()
     smmp.project_mt(ap32, aj, ax, Bp, R_host.indices, R_host.data, R_host.shape[1], threads)
     dt = time.perf_counter() - t0
+    # context: scipy's own A @ R (the library call the reference makes, one core, the CSR operand
+    # already converted) on the first 1M of those rows
+    import scipy.sparse as sp
+
+    n1 = min(n, 1_000_000)
+    A1 = sp.csr_matrix((ax[:ap32[n1]], aj[:ap32[n1]], ap32[:n1 + 1]), shape=(n1, R_host.shape[0]))
+    t1 = time.perf_counter()
+    _ = A1 @ R_host
+    ds = time.perf_counter() - t1
     return {"value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
             "sample": f"first {n} rows of the same synthetic workload; oracle/smmp.c (scipy csr_matmat_maxnnz + "
-                      f"csr_matmat restated) on {threads} threads, {dt:.2f}s wall"}
+                      f"csr_matmat restated) on {threads} threads, {dt:.2f}s wall",
+            "scipy_1core": {"value": n1 / ds, "unit": "rows/s", "rows": n1,
+                            "note": "scipy A @ R (csr_matmat), the reference's library call, 1 core"}}
 
 
 if __name__ == "__main__":
