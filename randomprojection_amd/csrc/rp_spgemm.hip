@@ -56,9 +56,6 @@ constexpr long kSpinLimit = 1l << 27;     // bounded waits (with s_sleep): secon
 
 // Diagnostic builds (-DRP_STAMPS, librp_diag.so only): thread 0 of each tile records
 // s_memrealtime (100 MHz) at stage boundaries into g_stamps[tile * 8 + k]. Never in librp.so.
-#ifndef RP_EXP
-#define RP_EXP 0  // timing experiments (scripts only): 1 no stage 2, 2 no products, 3 no look-back, 4 no writes
-#endif
 #ifdef RP_STAMPS
 __device__ unsigned long long* g_stamps;
 #define STAMP(k)                                                                                  \
@@ -568,7 +565,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     }
                     const uint32_t o0 = s_eoff[e], o1 = s_eoff[e + 1];
                     const uint32_t rtag = (uint32_t)s_erow[e] << 16;
-                    for (uint32_t t = 0; t < o1 - o0 && RP_EXP != 2; ++t) {
+                    for (uint32_t t = 0; t < o1 - o0; ++t) {
                         uint32_t col;
                         T v;
                         r_product<T>(R, mag, de, t, x[i], col, v);
@@ -583,8 +580,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 // ---- stage 2: flat over products. A product leads its column group if no earlier
                 // product of its row has that column (= scipy's first touch); the leader sums the
                 // group in sequence order starting from +0 (scipy: sums[k] = 0, then +=).
-                for (uint32_t q = tid; q < P_t && (RP_EXP == 1 || RP_EXP == 2); q += kBlock) s_rank[q] = 1;
-                for (uint32_t q = tid; q < P_t && RP_EXP != 1 && RP_EXP != 2; q += kBlock) {
+                for (uint32_t q = tid; q < P_t; q += kBlock) {
                     const uint32_t kr = s_pkr[q];
                     const uint32_t r = kr >> 16;
                     const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
@@ -623,7 +619,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 const uint32_t tile_c = lds_excl_scan(s_rank, P_t, s_wsum);
                 if (tid < 64) {
                     const unsigned long long g =
-                        RP_EXP == 3 ? 0ull : lookback_wave(states, tile, tile_c, ws, defer_polls);
+                        lookback_wave(states, tile, tile_c, ws, defer_polls);
                     if (tid == 0) s_off = g;
                 }
                 __syncthreads();
@@ -659,7 +655,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 }
                 uint16_t* __restrict__ pc = dfr.cols + (deferred ? s_pool : 0ull);
                 T* __restrict__ pv = reinterpret_cast<T*>(dfr.vals) + (deferred ? s_pool : 0ull);
-                if ((deferred || G + tile_c <= capacity) && RP_EXP != 4) {
+                if (deferred || G + tile_c <= capacity) {
                     // kept leaders write straight into the tile's contiguous output range
                     for (uint32_t q = tid; q < P_t; q += kBlock) {
                         const uint32_t rk = s_rank[q];
