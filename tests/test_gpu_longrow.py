@@ -1,0 +1,60 @@
+"""Long rows (configs[3] shape: ~100 entries, 30+ products per row; few rows per tile) against the
+oracle, bit for bit — both orders, f32/f64, uniform and power-law columns, empty rows, rows beyond
+the tile caps (exact slow path), frequent column collisions, forced and forbidden deferral."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import smmp
+from randomprojection_amd import Projector, srp_matrix as sm
+from test_gpu_parity import assert_same_csr, kdd_like, oracle_product
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(P, A, R):
+    want = oracle_product(A, R)
+    assert_same_csr(P.matmul(A), *want)
+    Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
+    assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
+
+
+@pytest.mark.parametrize("p", [1024, 4096])
+@pytest.mark.parametrize("powerlaw", [False, True])
+def test_longrow_vs_oracle(p, powerlaw):
+    rng = np.random.default_rng(40 + p + powerlaw)
+    m = 2_000_000
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    A = kdd_like(rng, 6000, m, mean=99, powerlaw=powerlaw, values="normal")
+    _check(Projector(R), A, R)
+
+
+def test_longrow_f64_empty_and_heavy_rows():
+    rng = np.random.default_rng(77)
+    m, p = 2_000_000, 4096
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123), dtype=np.float64)
+    A = sp.vstack([kdd_like(rng, 700, m, mean=80, values="normal", dtype=np.float64),
+                   sp.csr_matrix((40, m), dtype=np.float64),
+                   kdd_like(rng, 3, m, mean=900, values="normal", dtype=np.float64),  # heavy tiles
+                   kdd_like(rng, 500, m, mean=60, values="normal", dtype=np.float64)]).tocsr()
+    _check(Projector(R), A, R)
+
+
+def test_longrow_small_p_collisions():
+    """p = 64: a row's ~40 products collide often (sums of several products, cancellation to 0)."""
+    rng = np.random.default_rng(5)
+    m, p = 5000, 64
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    A = kdd_like(rng, 3000, m, mean=60, values="normal")
+    A.data[::7] = np.float32(1.0)
+    _check(Projector(R), A, R)
+
+
+@pytest.mark.parametrize("polls", ["0", "-1"])
+def test_longrow_deferral(polls, monkeypatch):
+    rng = np.random.default_rng(9)
+    m, p = 2_000_000, 1024
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    A = kdd_like(rng, 20_000, m, mean=99, powerlaw=True, values="normal")
+    monkeypatch.setenv("RP_DEFER_POLLS", polls)
+    _check(Projector(R), A, R)
