@@ -6,9 +6,11 @@ workload, inputs resident in HBM when timing starts (boundary 1 of SURVEY.md §8
        (per-row nnz 1 + Poisson(10), distinct uniform columns, values 1.0) on one MI355X.
   N>1: weak scaling — every rank projects its own 119,705,032-row shard (configs[2]'s
        row-sharding), R packed once on rank 0 and broadcast over RCCL; no collective in the loop.
+  --config kdd9x: configs[2] itself, 1,077,345,288 rows split over the ranks (strong scaling);
+  --config cfg4: configs[3], 200M x 10M power-law rows with exactly 100 nnz -> 1024.
 Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--dist uniform|powerlaw]
+    python bench.py [--config kdd|kdd9x|cfg4] [--gpus N] [--steps K] [--warmup W] [--rows R]
 """
 from __future__ import annotations
 
@@ -35,6 +37,13 @@ CONFIGS = {
             "workload": "configs[1]: KDD2012 train {rows} rows x {m} -> {p} per GPU, device-resident CSR in/out",
             "data": "synthetic KDD2012-shaped rows ({dist} columns, 1+Poisson(10) nnz/row, values 1.0), "
                     "R = SparseRandomProjection({p}, random_state=123) regenerated bit-identically"},
+    "kdd9x": {"rows": 1_077_345_288, "m": 54_686_452, "p": 4096, "dist": "uniform", "mean_extra": 10.0,
+              "cpu_sample_rows": 64_000_000, "strong": True,
+              "metric": "rows/sec projected (whole node), KDD2012 54.7M->4096 dims; achieved HBM GB/s",
+              "workload": "configs[2]: 9x KDD2012 train, 1,077,345,288 rows x {m} -> {p} row-sharded over the "
+                          "ranks ({rows} on this rank), device-resident CSR in/out",
+              "data": "synthetic KDD2012-shaped rows ({dist} columns, 1+Poisson(10) nnz/row, values 1.0), "
+                      "R = SparseRandomProjection({p}, random_state=123) regenerated bit-identically"},
     "cfg4": {"rows": 200_000_000, "m": 10_000_000, "p": 1024, "dist": "powerlaw", "mean_extra": -100.0,
              "cpu_sample_rows": 4_000_000,
              "metric": "rows/sec projected, synthetic power-law 200M x 10M (100 nnz/row) -> 1024; achieved HBM GB/s",
@@ -56,9 +65,10 @@ def algorithmic_bytes_per_row(a, rbar, c):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", choices=["kdd", "cfg4"], default="kdd",
-                    help="kdd: BASELINE configs[1] (default); cfg4: configs[3], 200M x 10M power-law rows, "
-                         "exactly 100 nnz/row -> 1024")
+    ap.add_argument("--config", choices=["kdd", "kdd9x", "cfg4"], default="kdd",
+                    help="kdd: BASELINE configs[1] (default, weak scaling: 119.7M rows per GPU); kdd9x: "
+                         "configs[2], 1.08B rows split over the GPUs (strong scaling); cfg4: configs[3], "
+                         "200M x 10M power-law rows, exactly 100 nnz/row -> 1024")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
@@ -87,6 +97,9 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    total_rows_cfg = args.rows
+    if cfg.get("strong"):  # a fixed total split over the ranks (contiguous shards)
+        args.rows = args.rows // world + (1 if rank < args.rows % world else 0)
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N>1 path on a one-GPU box only: every rank on cuda:0 over gloo
     # (RCCL refuses two ranks on one device); the driver's multi-GPU runs use neither
@@ -226,7 +239,7 @@ def main():
     gathers_per_s = nnz_a / (kernel_ms * 1e-3)
 
     if rank == 0:
-        total_rows = args.rows * world
+        total_rows = total_rows_cfg if cfg.get("strong") else args.rows * world
         out = {
             "metric": cfg["metric"],
             "value": total_rows / (t_max / args.steps),
@@ -236,7 +249,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": t_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if cfg.get("strong") else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": cfg["data"].format(dist=args.dist, p=args.p),
