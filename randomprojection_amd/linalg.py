@@ -82,8 +82,15 @@ class Vectors:
         return SparseVector(size, *args)
 
 
+_new_vector = SparseVector.__new__
+
+
 def make_vector(size, indices_sorted_i32, values_f64):
     """Vector from already sorted, deduplicated arrays (the GPU emits rows in ascending order)."""
     if _PySparkVector is not None:  # pragma: no cover
         return _PySparkVector(size, indices_sorted_i32, values_f64)
-    return SparseVector._trusted(size, indices_sorted_i32, values_f64)
+    v = _new_vector(SparseVector)
+    v.size = size
+    v.indices = indices_sorted_i32
+    v.values = values_f64
+    return v

@@ -40,22 +40,30 @@ def assemble_rows(rows):
     in float32) only if a row is not strictly increasing, which SparseVector rows never are."""
     ids, labels = [], []
     idx_list, val_list, lens = [], [], []
+    # bound methods: this loop runs once per row of the partition
+    ids_add, labels_add, idx_add, val_add, len_add = (ids.append, labels.append, idx_list.append,
+                                                      val_list.append, lens.append)
+    asarray, ndarray = np.asarray, np.ndarray
     has_label = False
     m = None
     for row in rows:
         has_label = "label" in row
-        ids.append(row["id"])
-        labels.append(row["label"] if has_label else None)
+        ids_add(row["id"])
+        labels_add(row["label"] if has_label else None)
         f = row["features"]
-        size = int(f.size)
-        if m is None:
-            m = size
-        elif size != m:
-            raise ValueError(f"blocks[{len(ids) - 1},:] has incompatible column dimensions. Got blocks[{len(ids) - 1},:].shape[1] == {size}, expected {m}.")
-        ii = np.asarray(f.indices)
-        idx_list.append(ii)
-        val_list.append(np.asarray(f.values))
-        lens.append(ii.size)
+        size = f.size
+        if size != m:
+            if m is None:
+                m = int(size)
+            elif int(size) != m:
+                raise ValueError(f"blocks[{len(ids) - 1},:] has incompatible column dimensions. Got blocks[{len(ids) - 1},:].shape[1] == {size}, expected {m}.")
+        ii = f.indices
+        if type(ii) is not ndarray:
+            ii = asarray(ii)
+        vv = f.values
+        idx_add(ii)
+        val_add(vv if type(vv) is ndarray else asarray(vv))
+        len_add(ii.size)
     if not ids:
         raise ValueError("blocks must be 2-D")
     indptr = np.zeros(len(ids) + 1, dtype=np.int64)
@@ -89,9 +97,11 @@ def random_project_mappartitions_function(rdd_row_iterator, local_csr_matrix):
     cx = Cx.astype(np.float64)
 
     def vectors():
-        for i in range(len(ids)):
-            s, e = Cp[i], Cp[i + 1]
+        bounds = Cp.tolist()  # Python ints: cheap per-row slicing
+        s = bounds[0]
+        for e in bounds[1:]:
             yield make_vector(p, cj[s:e], cx[s:e])
+            s = e
 
     if has_label:
         return zip(ids, labels, vectors())
