@@ -33,6 +33,9 @@
  *      random_project_map_function (localmode/randomProjection.py:15-36) and
  *      SparseRandomProjection.transform (sklearn/random_projection.py:801-824).
  *
+ *  rp_project
+ *      the same as begin + allocation + fetch in one call (the caller allocates in a callback).
+ *
  *  rp_libsvm_parse_device
  *      spark.read.format("libsvm").load(path, numFeatures=m)  code/clustermode/randomProjection.py:71
  *    libsvm text -> CSR on the GPU (Spark MLUtils.parseLibSVMRecord semantics).
@@ -164,6 +167,14 @@ int rp_project_host_begin(rp_projector* h, const rp_csr_in* a_host, int32_t orde
 int rp_result_fetch(rp_result* r, void* indptr, int32_t indptr_type, void* indices,
                     int32_t indices_type, void* data);
 int rp_result_free(rp_result* r);
+
+/* Fused convenience form of begin + fetch: computes C = A @ R for host A, then asks the caller to
+ * allocate the output through `alloc` (called once, with the exact n_rows and nnz; it returns 0 and
+ * sets host pointers of n_rows + 1 indptr entries and nnz indices/data entries, with their index
+ * types, or non-zero to abort with RP_ERR_NOMEM) and fills it. The data type is A's compute type. */
+typedef int (*rp_alloc_fn)(void* user, int64_t n_rows, int64_t nnz, void** indptr, int32_t* indptr_type,
+                           void** indices, int32_t* indices_type, void** data);
+int rp_project(rp_projector* h, const rp_csr_in* a_host, int32_t order, rp_alloc_fn alloc, void* user);
 
 /* Synthetic rows on the device: per-row nnz = 1 + Poisson(mean_extra), or exactly -mean_extra
  * when mean_extra < 0 (capped at max_row_nnz),

@@ -23,7 +23,7 @@ EXPORTS = (
     "rp_projector_create", "rp_projector_info_get", "rp_projector_export",
     "rp_projector_create_from_device", "rp_projector_destroy", "rp_pack_r_host",
     "rp_project_workspace_bytes", "rp_projector_set_staging", "rp_project_device",
-    "rp_project_host_begin", "rp_result_fetch", "rp_result_free",
+    "rp_project_host_begin", "rp_result_fetch", "rp_result_free", "rp_project",
     "rp_synth_rows_device", "rp_libsvm_parse_device",
 )
 
@@ -62,6 +62,13 @@ class CsrOut(ctypes.Structure):
         ("data", ctypes.c_void_p), ("capacity", ctypes.c_int64),
     ]
 
+
+# int (*rp_alloc_fn)(void* user, int64_t n_rows, int64_t nnz, void** indptr, int32_t* indptr_type,
+#                    void** indices, int32_t* indices_type, void** data)
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int32),
+                            ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int32),
+                            ctypes.POINTER(ctypes.c_void_p))
 
 _lib = None
 
@@ -104,6 +111,7 @@ def load(path: str = None):
         "rp_project_host_begin": (ctypes.c_int, [vp, P(CsrIn), i32, P(vp), P(i64)]),
         "rp_result_fetch": (ctypes.c_int, [vp, vp, i32, vp, i32, vp]),
         "rp_result_free": (ctypes.c_int, [vp]),
+        "rp_project": (ctypes.c_int, [vp, P(CsrIn), i32, ALLOC_FN, vp]),
         "rp_synth_rows_device": (ctypes.c_int, [ctypes.c_int, i64, i64, dbl, i32, i32, dbl, ctypes.c_uint64,
                                                 vp, i32, vp, vp, vp, P(i64)]),
         "rp_libsvm_parse_device": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, vp, vp, i32, vp, vp, i64, i64, vp,

@@ -1885,6 +1885,23 @@ int rp_result_free(rp_result* r) {
     return RP_OK;
 }
 
+int rp_project(rp_projector* h, const rp_csr_in* a, int32_t order, rp_alloc_fn alloc, void* user) {
+    if (!alloc) return fail(RP_ERR_INVALID, "NULL allocation callback");
+    rp_result* r = nullptr;
+    int64_t nnz = 0;
+    int rc = rp_project_host_begin(h, a, order, &r, &nnz);
+    if (rc) return rc;
+    void *ip = nullptr, *ix = nullptr, *dx = nullptr;
+    int32_t ipt = RP_I64, ixt = RP_I32;
+    if (alloc(user, r->n_rows, nnz, &ip, &ipt, &ix, &ixt, &dx) != 0) {
+        rp_result_free(r);
+        return fail(RP_ERR_NOMEM, "the allocation callback failed");
+    }
+    rc = rp_result_fetch(r, ip, ipt, ix, ixt, dx);
+    rp_result_free(r);
+    return rc;
+}
+
 int rp_synth_rows_device(int device, int64_t n_rows, int64_t m, double mean_extra,
                          int32_t max_row_nnz, int32_t dist, double zipf_s, uint64_t seed,
                          void* indptr, int32_t indptr_type, int32_t* indices, float* data,

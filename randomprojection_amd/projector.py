@@ -142,29 +142,36 @@ class Projector:
         n = len(indptr) - 1
         a = nat.CsrIn(n, nat.ptr(indptr).value, nat.idx_code(indptr.dtype), nat.ptr(aj).value,
                       nat.ptr(data).value, nat.val_code(T), int(indptr[-1] - indptr[0]) if n >= 0 else 0)
-        res = ctypes.c_void_p()
-        nnz = ctypes.c_int64(0)
         code = nat.RP_ORDER_SORTED if order == "sorted" else nat.RP_ORDER_SCIPY
-        with self._lock:
-            rc = self._lib.rp_project_host_begin(self._h, ctypes.byref(a), code, ctypes.byref(res), ctypes.byref(nnz))
-            if rc == nat.RP_ERR_INVALID:
-                raise ValueError(self._lib.rp_last_error().decode())
-            nat.check(rc)
+        out = {}
+
+        def alloc(_user, n_rows, k, p_indptr, p_ityp, p_indices, p_jtyp, p_data):
+            # rp_project's callback: the exact nnz is known, so scipy's index-dtype rule applies here
             try:
-                k = int(nnz.value)
-                if out_index_dtype is None:
-                    out_index_dtype = scipy_result_index_dtype((indptr, indices), k)
+                dt = out_index_dtype
+                if dt is None:
+                    dt = scipy_result_index_dtype((indptr, indices), k)
                     if self.r_index_dtype == np.int64:
-                        out_index_dtype = np.dtype(np.int64)
-                out_index_dtype = np.dtype(out_index_dtype)
-                Cp = np.empty(n + 1, dtype=out_index_dtype)
-                Cj = np.empty(k, dtype=out_index_dtype)
-                Cx = np.empty(k, dtype=T)
-                nat.check(self._lib.rp_result_fetch(res, nat.ptr(Cp), nat.idx_code(out_index_dtype), nat.ptr(Cj),
-                                                    nat.idx_code(out_index_dtype), nat.ptr(Cx)))
-            finally:
-                self._lib.rp_result_free(res)
-        return Cp, Cj, Cx
+                        dt = np.dtype(np.int64)
+                dt = np.dtype(dt)
+                out["Cp"] = np.empty(n_rows + 1, dtype=dt)
+                out["Cj"] = np.empty(k, dtype=dt)
+                out["Cx"] = np.empty(k, dtype=T)
+                p_indptr[0] = out["Cp"].ctypes.data
+                p_indices[0] = out["Cj"].ctypes.data if k else None
+                p_data[0] = out["Cx"].ctypes.data if k else None
+                p_ityp[0] = p_jtyp[0] = nat.idx_code(dt)
+                return 0
+            except Exception:  # noqa: BLE001 - reported as RP_ERR_NOMEM by the library
+                return 1
+
+        cb = nat.ALLOC_FN(alloc)
+        with self._lock:
+            rc = self._lib.rp_project(self._h, ctypes.byref(a), code, cb, None)
+        if rc == nat.RP_ERR_INVALID:
+            raise ValueError(self._lib.rp_last_error().decode())
+        nat.check(rc)
+        return out["Cp"], out["Cj"], out["Cx"]
 
     def matmul(self, A, order: str = "scipy"):
         """``A @ R`` for sparse A, returning what scipy returns (container of A's class)."""
