@@ -574,6 +574,10 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     }
                 }
             }
+            // stage 2 reads keys in aligned groups of four: pad the last group with a key no product
+            // has (rows < 256), so stale LDS from an earlier tile can never match
+            if (tid < 4 && P_t + tid < (uint32_t)caps.cap_p && ((P_t + tid) >> 2) == (P_t >> 2))
+                s_pkr[P_t + tid] = 0xffffffffu;
             __syncthreads();
             STAMP(3);
             if (!s_heavy) {  // uniform
@@ -584,29 +588,35 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     const uint32_t kr = s_pkr[q];
                     const uint32_t r = kr >> 16;
                     const uint32_t rs = s_rowS[r], re = s_rowS[r + 1];
-                    // keys are read four at a time (one ds_read_b128 from a 16-byte aligned group,
-                    // out-of-range lanes masked): a quarter of the dependent LDS round trips
+                    // keys are read four at a time (one ds_read_b128 per 16-byte aligned group).
+                    // A key holds the row, so keys of other rows never match: before q only
+                    // "earlier" matters for the leader test, after q only "later" for the sum.
                     const uint4* pk4 = reinterpret_cast<const uint4*>(s_pkr);
+                    const uint32_t gq = q >> 2, oq = q & 3u;
                     bool leader = true;
-                    for (uint32_t g = rs >> 2; g <= (q - 1) >> 2 && q > rs; ++g) {
+                    for (uint32_t g = rs >> 2; g < gq; ++g) {
                         const uint4 k4 = pk4[g];
-                        const uint32_t b = g << 2;
-                        leader &= !((k4.x == kr) & (b >= rs) & (b < q));
-                        leader &= !((k4.y == kr) & (b + 1 >= rs) & (b + 1 < q));
-                        leader &= !((k4.z == kr) & (b + 2 >= rs) & (b + 2 < q));
-                        leader &= !((k4.w == kr) & (b + 3 >= rs) & (b + 3 < q));
+                        leader &= (k4.x != kr) & (k4.y != kr) & (k4.z != kr) & (k4.w != kr);
                     }
+                    const uint4 kq = pk4[gq];
+                    leader &= !(((oq > 0u) & (kq.x == kr)) | ((oq > 1u) & (kq.y == kr)) |
+                                ((oq > 2u) & (kq.z == kr)));
                     uint16_t flag = 0;
                     if (leader) {
                         T sum = tadd<T>(T(0), s_pv[q]);
-                        for (uint32_t g = (q + 1) >> 2; (g << 2) < re; ++g) {
+                        // the rest of q's group, then whole groups up to the row end, in order
+                        if ((oq < 1u) & (kq.y == kr)) sum = tadd<T>(sum, s_pv[(gq << 2) + 1]);
+                        if ((oq < 2u) & (kq.z == kr)) sum = tadd<T>(sum, s_pv[(gq << 2) + 2]);
+                        if ((oq < 3u) & (kq.w == kr)) sum = tadd<T>(sum, s_pv[(gq << 2) + 3]);
+                        for (uint32_t g = gq + 1; (g << 2) < re; ++g) {
                             const uint4 k4 = pk4[g];
-                            const uint32_t b = g << 2;
-                            // in sequence order; only matching products (same row and column) add
-                            if (k4.x == kr && b > q && b < re) sum = tadd<T>(sum, s_pv[b]);
-                            if (k4.y == kr && b + 1 > q && b + 1 < re) sum = tadd<T>(sum, s_pv[b + 1]);
-                            if (k4.z == kr && b + 2 > q && b + 2 < re) sum = tadd<T>(sum, s_pv[b + 2]);
-                            if (k4.w == kr && b + 3 > q && b + 3 < re) sum = tadd<T>(sum, s_pv[b + 3]);
+                            if ((k4.x == kr) | (k4.y == kr) | (k4.z == kr) | (k4.w == kr)) {  // rare
+                                const uint32_t b = g << 2;
+                                if (k4.x == kr) sum = tadd<T>(sum, s_pv[b]);
+                                if (k4.y == kr) sum = tadd<T>(sum, s_pv[b + 1]);
+                                if (k4.z == kr) sum = tadd<T>(sum, s_pv[b + 2]);
+                                if (k4.w == kr) sum = tadd<T>(sum, s_pv[b + 3]);
+                            }
                         }
                         s_pv[q] = sum;  // position q is read by no other leader (column differs)
                         flag = sum != T(0) ? 1 : 0;
