@@ -224,6 +224,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, Ap, Aj, Ax, R_host)
+    # the timed output, checked after the clock: a seeded sample of rows against the oracle (bit for
+    # bit), and CSR well-formedness of the whole result on the device
+    check = verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host) if rank == 0 else None
 
     traffic = None
     if os.path.exists(args.traffic_json):
@@ -269,6 +272,7 @@ def main():
                          "gathers_G_per_s": gathers_per_s / 1e9,
                          "frac_of_random_line_ceiling": gathers_per_s / RANDOM_LINE_CEILING},
             "cpu_baseline": cpu,
+            "verified": check,
             "r_setup_s": t_r,
             "r_broadcast_ms": t_bcast * 1e3,
             "tiles": n_tiles_run, "deferred_tiles": n_deferred,
@@ -276,6 +280,39 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host, n_sample=4096):
+    """After the timed region: Cp monotone from 0 to nnz, every column in [0, p), and a seeded
+    sample of rows (spread over the whole matrix) equal to the oracle's restatement of scipy's
+    csr_matmat, bit for bit (indices in scipy's per-row order and value bits)."""
+    import scipy.sparse as sp
+    import torch
+
+    from oracle import smmp
+
+    cp = Cp.to(torch.int64)
+    ok_ptr = bool(cp[0].item() == 0 and cp[-1].item() == nnz_c and torch.all(cp[1:] >= cp[:-1]).item())
+    cj = Cj[:nnz_c]
+    ok_cols = bool(nnz_c == 0 or (int(cj.min().item()) >= 0 and int(cj.max().item()) < args.p))
+    rng = np.random.default_rng(20261016)
+    rows = np.sort(rng.choice(args.rows, size=min(n_sample, args.rows), replace=False))
+    r_t = torch.as_tensor(rows, device=Ap.device)
+    s0, s1 = Ap[r_t].to(torch.int64).cpu().numpy(), Ap[r_t + 1].to(torch.int64).cpu().numpy()
+    c0, c1 = cp[r_t].cpu().numpy(), cp[r_t + 1].cpu().numpy()
+
+    def take(t, lo, hi):  # the sampled rows' segments of a device array, gathered on the device
+        idx = np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)]).astype(np.int64)
+        return t[torch.as_tensor(idx, device=t.device)].cpu().numpy()
+
+    ptr = np.concatenate([[0], np.cumsum(s1 - s0)])
+    A = sp.csr_matrix((take(Ax, s0, s1), take(Aj, s0, s1), ptr), shape=(rows.size, args.m))
+    Wp, Wj, Wx, _, _ = smmp.matmat(A, R_host)
+    got_ptr = np.concatenate([[0], np.cumsum(c1 - c0)])
+    same = (np.array_equal(got_ptr, Wp) and np.array_equal(take(Cj, c0, c1), Wj)
+            and np.array_equal(take(Cx, c0, c1).view(np.uint32), Wx.view(np.uint32)))
+    return {"sample_rows": int(rows.size), "sample_bitexact_vs_oracle": bool(same),
+            "indptr_ok": ok_ptr, "columns_ok": ok_cols}
 
 
 def cpu_baseline(args, Ap, Aj, Ax, R_host):
