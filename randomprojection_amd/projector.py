@@ -22,6 +22,7 @@ import numpy as np
 import scipy.sparse as sp
 
 from . import _native as nat
+from . import hostmem
 
 __all__ = ["Projector", "get_projector", "scipy_result_index_dtype"]
 
@@ -154,9 +155,11 @@ class Projector:
                     if self.r_index_dtype == np.int64:
                         dt = np.dtype(np.int64)
                 dt = np.dtype(dt)
-                out["Cp"] = np.empty(n_rows + 1, dtype=dt)
-                out["Cj"] = np.empty(k, dtype=dt)
-                out["Cx"] = np.empty(k, dtype=T)
+                # recycled, already-faulted host memory: first-touch faults of fresh arrays would
+                # cost more than the copies themselves (hostmem.py)
+                out["Cp"] = hostmem.empty(n_rows + 1, dt)
+                out["Cj"] = hostmem.empty(k, dt)
+                out["Cx"] = hostmem.empty(k, T)
                 p_indptr[0] = out["Cp"].ctypes.data
                 p_indices[0] = out["Cj"].ctypes.data if k else None
                 p_data[0] = out["Cx"].ctypes.data if k else None

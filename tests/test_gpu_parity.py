@@ -235,6 +235,32 @@ def test_index64_inputs_follow_scipy_dtype_rule():
         assert_same_csr(C, Cr.indptr, Cr.indices, Cr.data)
 
 
+@pytest.mark.parametrize("threads", ["4", "0"])
+def test_large_host_fetch_pipelined(threads, monkeypatch):
+    """Outputs past 16 MB are downloaded in chunks while helper threads pre-fault the fresh numpy
+    destinations (RP_HOST_THREADS=0: plain copies); every index/value dtype combination."""
+    monkeypatch.setenv("RP_HOST_THREADS", threads)  # 4 = the default
+    rng = np.random.default_rng(21)
+    m, p, n = 2_000_000, 4096, 1_500_000
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    k = 1 + rng.poisson(10, size=n)
+    indptr = np.concatenate([[0], np.cumsum(k)]).astype(np.int64)
+    idx = rng.integers(0, m, size=int(indptr[-1])).astype(np.int32)
+    val = rng.standard_normal(idx.size).astype(np.float32)
+    A = sp.csr_matrix((val, idx, indptr), shape=(n, m))
+    Cp, Cj, Cx = oracle_product(A, R)
+    assert Cj.size * 8 > (16 << 20)
+    P = Projector(R)
+    for dt in (np.int32, np.int64):
+        ip, ix, dx = P.project_arrays(A.indptr, A.indices, A.data, out_index_dtype=dt)
+        assert ip.dtype == ix.dtype == dt
+        assert np.array_equal(ip, Cp) and np.array_equal(ix, Cj) and same_bits(dx, Cx)
+    ip, ix, dx = P.project_arrays(A.indptr, A.indices, A.data.astype(np.float64))
+    # (A.astype would canonicalise A's unsorted, duplicated rows: build the f64 twin from the arrays)
+    C64 = oracle_product(sp.csr_matrix((A.data.astype(np.float64), A.indices, A.indptr), shape=A.shape), R)
+    assert np.array_equal(ip, C64[0]) and np.array_equal(ix, C64[1]) and same_bits(dx, C64[2])
+
+
 @pytest.mark.slow
 def test_full_kdd_R_vs_oracle():
     """The recipe's own R (54,686,452 x 4096, random_state=123) on 60k KDD-shaped rows."""

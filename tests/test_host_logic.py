@@ -63,3 +63,30 @@ def test_result_index_dtype_rule():
     assert scipy_result_index_dtype((i32, i32), 10) == np.int32
     assert scipy_result_index_dtype((i32, i64), 10) == np.int64
     assert scipy_result_index_dtype((i32, i32), 2**31) == np.int64
+
+
+def test_hostmem_pool_recycles_only_dead_arrays(monkeypatch):
+    """Pooled result arrays (hostmem.empty) are plain numpy arrays; a mapping goes back to the pool
+    only after the array and every view of it are gone, and idle memory is bounded."""
+    import gc
+    from randomprojection_amd import hostmem
+
+    a = hostmem.empty(3_000_000, np.int32)
+    assert a.shape == (3_000_000,) and a.dtype == np.int32 and a.flags.writeable and a.flags.c_contiguous
+    a[:] = 5
+    v = a[100:200]
+    addr = a.ctypes.data
+    del a
+    gc.collect()
+    b = hostmem.empty(3_000_000, np.int32)          # the first mapping is still held by v
+    assert b.ctypes.data != addr and np.all(v == 5)
+    del v
+    gc.collect()
+    c = hostmem.empty(2_800_000, np.float32)        # best fit: the recycled mapping
+    assert c.ctypes.data == addr
+    assert hostmem.empty(10, np.int64).shape == (10,)   # small requests: np.empty
+    monkeypatch.setenv("RP_HOST_POOL_BYTES", "0")
+    del b, c
+    gc.collect()
+    st = hostmem.pool_stats()
+    assert st["idle_bytes"] == 0 and st["unmapped"] >= 2
