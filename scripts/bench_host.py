@@ -65,20 +65,26 @@ def main():
              "features": SparseVector(sm.KDD_M, B.indices[B.indptr[i]:B.indptr[i + 1]],
                                       B.data[B.indptr[i]:B.indptr[i + 1]].astype(np.float64))}
             for i in range(B.shape[0])]
+    # first partition: includes packing + uploading R (get_projector caches it per R object);
+    # later partitions of the same broadcast R find it resident
+    t0 = time.perf_counter()
+    out = list(random_project_mappartitions_function(iter(rows), R))
+    cold_s = time.perf_counter() - t0
     t0 = time.perf_counter()
     out = list(random_project_mappartitions_function(iter(rows), R))
     dropin_s = time.perf_counter() - t0
     assert len(out) == len(rows)
     # the reference's own recipe restated with the same scipy calls (oracle/recipe.py), 1 core,
-    # on the same rows and the recipe's CSC operand (components_.T)
+    # on the same partition and the recipe's CSC operand (components_.T); one call = one partition,
+    # so its per-call conversion of R (scipy _compressed.py:564) is paid once, as in the reference
     from oracle.recipe import recipe_partition
 
-    n_ref = min(args.part_rows, 20_000)
+    n_ref = args.part_rows
     Rcsc = R.tocsc()
     recipe_partition(rows[:100], Rcsc)
     t0 = time.perf_counter()
     ref_out = recipe_partition(rows[:n_ref], Rcsc)
-    ref_s = (time.perf_counter() - t0) * args.part_rows / n_ref
+    ref_s = time.perf_counter() - t0
     for a, b in zip(ref_out[:200], out[:200]):  # same answer, checked on a prefix
         assert a[0] == b[0] and np.array_equal(a[2].indices, b[2].indices)
         assert np.array_equal(a[2].values, b[2].values)
@@ -112,11 +118,14 @@ def main():
         "boundary": "host CSR in -> host CSR out (PCIe-inclusive)",
         "rows": args.rows, "host_rows_per_s": host_rows_s, "nnz_out": int(C.nnz),
         "dropin_partition": {"rows": args.part_rows, "rows_per_s": args.part_rows / dropin_s,
-                             "us_per_row": dropin_s / args.part_rows * 1e6},
+                             "us_per_row": dropin_s / args.part_rows * 1e6,
+                             "first_partition_s": cold_s,
+                             "note": "R resident (second partition); first_partition_s includes packing and uploading R"},
         "recipe_restatement_1core": {"rows_per_s": args.part_rows / ref_s, "us_per_row": ref_s / args.part_rows * 1e6,
                                      "rows_timed": n_ref,
                                      "note": "oracle/recipe.py: the reference partition function's own scipy calls "
-                                             "(per-row coo->csr, vstack, CSR@CSC dot, per-row Vectors.sparse), 1 core"},
+                                             "(per-row coo->csr, vstack, CSR@CSC dot incl. its R conversion, "
+                                             "per-row Vectors.sparse), 1 core, one whole partition"},
         "dropin_speedup_vs_recipe": (ref_s / args.part_rows) / (dropin_s / args.part_rows),
         "libsvm_text_to_host_csr": {"rows": n_txt, "text_bytes": len(text), "rows_per_s": n_txt / txt_s,
                                     "text_GB_per_s": len(text) / txt_s / 1e9,
