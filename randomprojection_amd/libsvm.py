@@ -20,6 +20,7 @@ import numpy as np
 import scipy.sparse as sp
 
 from . import _native as nat
+from . import hostmem
 
 __all__ = ["parse_device", "parse_bytes", "iter_chunks", "load_libsvm", "project_libsvm", "partition_ids"]
 
@@ -153,5 +154,16 @@ def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order
             Cj = torch.empty(e.nnz, dtype=torch.int32, device=Cp.device)
             Cx = torch.empty(e.nnz, dtype=torch.float32, device=Cp.device)
             k = projector.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=order, nnz_a=int(Aj.numel()))
-        C = sp.csr_matrix((Cx[:k].cpu().numpy(), Cj[:k].cpu().numpy(), Cp.cpu().numpy()), shape=(rows, projector.p))
-        yield partition_ids(ci, rows), labels.cpu().numpy(), C
+        if k < 2**31:  # the index dtype scipy's csr_matrix settles on
+            Cp = Cp.to(torch.int32)
+        C = sp.csr_matrix((_download(Cx[:k]), _download(Cj[:k]), _download(Cp)), shape=(rows, projector.p))
+        yield partition_ids(ci, rows), _download(labels), C
+
+
+def _download(t):
+    """Device tensor -> host array in recycled, already-faulted memory (hostmem.py)."""
+    import torch
+
+    out = hostmem.empty(t.numel(), torch.empty(0, dtype=t.dtype).numpy().dtype)
+    torch.from_numpy(out).copy_(t)
+    return out
