@@ -445,8 +445,12 @@ __device__ __forceinline__ uint32_t lds_excl_scan(V* a, uint32_t n, uint32_t* s_
 // from W: S[q] = entry << 20 | column-in-bucket and D[q] = W32 word of that column, for the tile's
 // entries in bucket order (q relative to Ap[0]). Two coalesced 4-byte reads per entry replace one
 // random 128-B line fill.
-template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED>
-__global__ void __launch_bounds__(kBlock)
+// WPE: minimum waves per SIMD the register allocation must allow (1 = unconstrained: 76 VGPRs,
+// 6 waves). 7 is used when the tile's LDS leaves room for 7 tiles per CU (configs[3]: 29-row tiles,
+// 19.6 KB; f32 packed, 71 VGPRs, no spills): 252 -> 235 ms. KDD2012 tiles (26.9 KB) are
+// LDS-limited to 5 per CU, where the tighter allocation measured 3% slower.
+template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED, int WPE = 1>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE)))
 spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict__ Ap,
                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
                        OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
@@ -1200,18 +1204,24 @@ int defer_polls_setting(const Caps& caps) {
     return e ? atoi(e) : (caps.rpt >= 128 ? kDeferPolls : 4 * kDeferPolls);
 }
 
-template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED>
+template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED, int WPE = 1>
 int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
                 int order, Workspace* ws, unsigned n_tiles, const Plan& pl, size_t lds,
                 hipStream_t st, const uint32_t* S, const T* SX, const uint32_t* D) {
-    HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED>,
+    if constexpr (WPE == 1 && !STAGED && std::is_same<T, float>::value && std::is_same<RL, PackedR>::value) {
+        // 7 tiles per CU fit the LDS (static arrays ~1.6 KB per tile): take the 7-wave build
+        if (lds + 2048 <= 160 * 1024 / 7)
+            return launch_main<T, IP, OP, OI, RL, STAGED, 7>(R, mag, h, a, c, order, ws, n_tiles, pl, lds,
+                                                             st, S, SX, D);
+    }
+    HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED, WPE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     char* base = reinterpret_cast<char*>(ws);
     DeferSpace dfr{reinterpret_cast<unsigned int*>(base + pl.dlist),
                    reinterpret_cast<unsigned long long*>(base + pl.pofs),
                    reinterpret_cast<uint16_t*>(base + pl.dhdr), reinterpret_cast<uint16_t*>(base + pl.pcols),
                    reinterpret_cast<unsigned char*>(base + pl.pvals), pl.pool_cap};
-    hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED>), dim3(n_tiles), dim3(kBlock), lds, st,
+    hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED, WPE>), dim3(n_tiles), dim3(kBlock), lds, st,
                        R, mag, (int)h->p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
                        (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order,
