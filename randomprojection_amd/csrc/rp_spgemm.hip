@@ -1214,6 +1214,8 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
             return launch_main<T, IP, OP, OI, RL, STAGED, 7>(R, mag, h, a, c, order, ws, n_tiles, pl, lds,
                                                              st, S, SX, D);
     }
+    if (const char* pad = STAGED ? nullptr : getenv("RP_DEBUG_LDS_PAD"))  // residency experiments
+        lds = std::min<size_t>(lds + (size_t)atol(pad), 160 * 1024 - 2048);
     HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED, WPE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     char* base = reinterpret_cast<char*>(ws);
