@@ -15,6 +15,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -228,14 +229,20 @@ def main():
     # bit), and CSR well-formedness of the whole result on the device
     check = verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host) if rank == 0 else None
 
-    traffic = None
-    if os.path.exists(args.traffic_json):
+    # rocprofv3 PMC results of an earlier profiling session of this same workload (profiles/):
+    # HBM bytes per step and the L2 hit rate of the main kernel (= on the R gathers, which are
+    # >90% of its reads); the explicit --traffic-json first, then any profiles/*traffic*.json
+    traffic, l2_hit, traffic_file = None, None, None
+    cands = [args.traffic_json] + sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
+    for f in cands:
         try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("rows") == args.rows and tj.get("dist") == args.dist:
-                traffic = tj.get("hbm_bytes_per_launch")
+            tj = json.load(open(f))
         except Exception:  # noqa: BLE001
-            traffic = None
+            continue
+        if tj.get("rows") == args.rows and tj.get("dist") == args.dist:
+            traffic, l2_hit = tj.get("hbm_bytes_per_launch"), tj.get("l2_hit_rate_main_kernel")
+            traffic_file = os.path.relpath(f, ROOT)
+            break
     # the ceiling that binds this kernel: one random R-descriptor gather per A entry, each a full
     # 128-B line fill; measured on MI355X at ~55 G random lines/s for any table from 32 MB to 2 GB,
     # any load flavour or allocation (profiles/r01_probe_gather_*.json)
@@ -263,7 +270,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kernel_ms, "bytes_per_row": b_row,
                          "model": "B_row=(4+8a)+a(8+8r)+(4+8c)", "a": a, "r": rbar, "c": c,
-                         "traffic_source": "rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per step, profiles/",
+                         "traffic_source": f"rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per step, {traffic_file}",
+                         "l2_hit_rate_r_gathers": l2_hit,
                          "step_kernels": ["spgemm_lookback_kernel", "defer_copy_kernel"] +
                                          (["stage_partition_kernel", "stage_gather_kernel"]
                                           if args.staging == "on" else []),

@@ -93,6 +93,8 @@ def main():
     if "hbm_bytes" in summary["step"]:
         json.dump({"tag": args.tag, "rows": args.rows, "dist": args.dist,
                    "hbm_bytes_per_launch": summary["step"]["hbm_bytes"],
+                   "l2_hit_rate_main_kernel": summary["kernels"].get("spgemm_lookback_kernel", {}).get("l2_hit_rate"),
+                   "l2_hit_rate_step": summary["step"].get("l2_hit_rate"),
                    "note": "per projection step (all kernels of rp_project_device)",
                    "source": f"profiles/{args.tag}_summary.json"},
                   open(os.path.join(prof, "traffic_latest.json"), "w"), indent=1)
