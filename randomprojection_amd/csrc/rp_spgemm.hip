@@ -225,7 +225,8 @@ __device__ unsigned long long wave_sum_u64(unsigned long long v) {
 // is already there (defer_copy_kernel).
 __device__ unsigned long long lookback_wave(unsigned long long* states, unsigned int tile,
                                             unsigned long long agg, Workspace* ws,
-                                            long max_polls = -1, bool publish_agg = true) {
+                                            long max_polls = -1, bool publish_agg = true,
+                                            long max_ticks = 0) {
     const int lane = threadIdx.x & 63;
     if (tile == 0) {
         if (lane == 0)
@@ -237,6 +238,7 @@ __device__ unsigned long long lookback_wave(unsigned long long* states, unsigned
     unsigned long long excl = 0;
     long base = (long)tile - 1;  // nearest predecessor not yet summed
     long spins = 0;
+    const unsigned long long t0 = max_ticks > 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
     while (true) {
         const long idx = base - lane;
         unsigned long long st = idx >= 0 ? __hip_atomic_load(&states[idx], __ATOMIC_RELAXED,
@@ -252,7 +254,9 @@ __device__ unsigned long long lookback_wave(unsigned long long* states, unsigned
             base -= 64;
             continue;
         }
-        if (max_polls >= 0 && spins >= max_polls) return ~0ull;  // defer: aggregate stays published
+        if (max_polls >= 0 && (max_ticks > 0 ? (long)(__builtin_amdgcn_s_memrealtime() - t0) >= max_ticks
+                                             : spins >= max_polls))
+            return ~0ull;  // defer: aggregate stays published
         if (++spins > kSpinLimit) {
             if (lane == 0) atomicOr(&ws->error, 1u);
             break;
@@ -457,7 +461,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                        unsigned long long capacity, Caps caps, int order, Workspace* ws,
                        unsigned int n_tiles, const uint32_t* __restrict__ S,
                        const T* __restrict__ SX, const uint32_t* __restrict__ D,
-                       DeferSpace dfr, int defer_polls) {
+                       DeferSpace dfr, int defer_polls, int defer_ticks) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ uint16_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative, <= cap_a)
     __shared__ uint16_t s_rowS[kBlock + 1];    // row -> first product
@@ -634,7 +638,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 const uint32_t tile_c = lds_excl_scan(s_rank, P_t, s_wsum);
                 if (tid < 64) {
                     const unsigned long long g =
-                        lookback_wave(states, tile, tile_c, ws, defer_polls);
+                        lookback_wave(states, tile, tile_c, ws, defer_polls, true, defer_ticks);
                     if (tid == 0) s_off = g;
                 }
                 __syncthreads();
@@ -1149,7 +1153,9 @@ struct Plan {
 };
 
 constexpr unsigned kDeferCopyGrid = 32768;  // copy workgroups (grid-stride over the deferred list)
-constexpr int kDeferPolls = 2;                 // look-back polls before a tile defers its output
+constexpr int kDeferPolls = 4;                 // polls before a 256-row tile defers (time budget off)
+constexpr int kDeferPollsShort = 8;            // ... and before a tile of fewer than 128 rows does
+constexpr int kDeferTicks = 800;               // 256-row tiles: wait budget, 8 us (defer_ticks_setting)
 constexpr bool kStageAuto = false;              // auto picks staging (off until it measures faster)
 constexpr int64_t kStageMinNnz = 1 << 22;      // auto: stage only launches this large
 constexpr int64_t kStageMinTable = 64ll << 20;  // ... and only a W past L2/MALL-friendly sizes
@@ -1196,12 +1202,27 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
     return pl;
 }
 
-// Polls before a tile defers. Measured optimum differs with the tile shape: 2 on configs[1]
-// (256-row tiles whose random-gather latency varies widely: 27.7 ms vs 32.7 waiting), 8 on
-// configs[3] (29-row tiles of 100-nnz rows hitting L2: 268 ms vs 285 waiting, 325 at 2 polls).
+// Polls before a tile defers. Measured optimum differs with the tile shape and the gather pattern
+// (DESIGN.md §3d): configs[1] uniform columns 2/3/4/5/6/8 polls 28.0/27.9/27.9/27.9/28.1/28.5 ms,
+// 32.7 waiting (random-gather latency varies widely); the same rows with power-law columns
+// 2/4/8/12/16 polls 22.6/21.5/20.1/19.6/19.6 ms, 19.8 waiting; configs[3] (29-row tiles of 100-nnz
+// rows hitting L2) 268 ms at 8, 285 waiting, 325 at 2. 4 for 256-row tiles is the best uniform
+// setting and 5% better than 2 on power-law rows.
+// 256-row tiles wait for their prefix up to a time budget (s_memrealtime ticks, 100 MHz) rather
+// than a poll count: a poll takes longer when the random gathers congest memory, so a time budget
+// waits fewer polls where predecessors are slow and more where they finish quickly. Measured
+// (DESIGN.md §3d): 8 us gives configs[1] uniform 27.95 ms (polls: 27.9 at best) and power-law
+// 19.4 ms (polls 4: 21.0, never deferring: 19.8); 12 us already costs uniform 29.1 ms.
+// RP_DEFER_POLLS (tests, tuning) turns the time budget off; RP_DEFER_TICKS overrides it.
+int defer_ticks_setting(const Caps& caps) {
+    if (const char* e = getenv("RP_DEFER_TICKS")) return std::max(atoi(e), 0);
+    if (getenv("RP_DEFER_POLLS")) return 0;
+    return caps.rpt >= 128 ? kDeferTicks : 0;
+}
+
 int defer_polls_setting(const Caps& caps) {
     const char* e = getenv("RP_DEFER_POLLS");  // tests and tuning: -1 never defer, 0 defer at once
-    return e ? atoi(e) : (caps.rpt >= 128 ? kDeferPolls : 4 * kDeferPolls);
+    return e ? atoi(e) : (caps.rpt >= 128 ? kDeferPolls : kDeferPollsShort);
 }
 
 template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED, int WPE = 1>
@@ -1227,7 +1248,8 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
                        R, mag, (int)h->p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
                        (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order,
-                       ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting(pl.caps) : -1);
+                       ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting(pl.caps) : -1,
+                       pl.defer ? defer_ticks_setting(pl.caps) : 0);
     HIP_TRY(hipGetLastError());
     if (pl.defer) {
         hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, kDeferCopyGrid)), dim3(kBlock), 0,

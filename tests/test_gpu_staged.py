@@ -135,3 +135,16 @@ def test_deferred_output_tiles(R2m, polls, staged, monkeypatch):
     assert_same_csr(P.matmul(A), *want)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
+
+
+@pytest.mark.parametrize("ticks", ["1", "300", "100000"])
+def test_deferred_output_time_budget(R2m, ticks, monkeypatch):
+    """256-row tiles wait up to RP_DEFER_TICKS s_memrealtime ticks (default 800 = 8 us) before
+    parking their output: every budget gives the oracle's bits."""
+    monkeypatch.setenv("RP_DEFER_TICKS", ticks)
+    rng = np.random.default_rng(57)
+    m = R2m.shape[0]
+    A = sp.vstack([kdd_like(rng, 25_000, m, values="normal"), sp.csr_matrix((200, m), dtype=np.float32),
+                   kdd_like(rng, 25_000, m, powerlaw=True, values="normal")]).tocsr()
+    want = oracle_product(A, R2m)
+    assert_same_csr(Projector(R2m).matmul(A), *want)
