@@ -231,7 +231,8 @@ def main():
 
     # rocprofv3 PMC results of an earlier profiling session of this same workload (profiles/):
     # HBM bytes per step and the L2 hit rate of the main kernel (= on the R gathers, which are
-    # >90% of its reads); the explicit --traffic-json first, then any profiles/*traffic*.json
+    # >90% of its reads); the explicit --traffic-json first, then any profiles/*traffic*.json (all
+    # profiled in direct mode: none applies to a staged run)
     traffic, l2_hit, traffic_file = None, None, None
     cands = [args.traffic_json] + sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
     for f in cands:
@@ -239,7 +240,7 @@ def main():
             tj = json.load(open(f))
         except Exception:  # noqa: BLE001
             continue
-        if tj.get("rows") == args.rows and tj.get("dist") == args.dist:
+        if tj.get("rows") == args.rows and tj.get("dist") == args.dist and args.staging != "on":
             traffic, l2_hit = tj.get("hbm_bytes_per_launch"), tj.get("l2_hit_rate_main_kernel")
             traffic_file = os.path.relpath(f, ROOT)
             break
