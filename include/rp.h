@@ -36,6 +36,12 @@
  *  rp_project
  *      the same as begin + allocation + fetch in one call (the caller allocates in a callback).
  *
+ *  rp_project_stream
+ *      the same product for a host matrix of any size, cut into chunks of rows (the recipe's
+ *      partitions, code/clustermode/randomProjection.py:107-110, each projected by the partition
+ *      function, :28-54) whose upload, projection and download overlap; results go straight into
+ *      caller host arrays at their final CSR positions (BASELINE configs[1]: chunked row streaming).
+ *
  *  rp_libsvm_parse_device
  *      spark.read.format("libsvm").load(path, numFeatures=m)  code/clustermode/randomProjection.py:71
  *    libsvm text -> CSR on the GPU (Spark MLUtils.parseLibSVMRecord semantics).
@@ -175,6 +181,22 @@ int rp_result_free(rp_result* r);
 typedef int (*rp_alloc_fn)(void* user, int64_t n_rows, int64_t nnz, void** indptr, int32_t* indptr_type,
                            void** indices, int32_t* indices_type, void** data);
 int rp_project(rp_projector* h, const rp_csr_in* a_host, int32_t order, rp_alloc_fn alloc, void* user);
+
+/* Chunked host streaming (boundary 2): C = A @ R for host CSR A of any size into caller host
+ * arrays c_host (indptr: n_rows + 1 entries of indptr_type; indices/data: capacity entries; data in
+ * the compute type). Rows go in chunks of chunk_rows (0 = 4M): chunk k+1's upload, chunk k's
+ * kernels and chunk k-1's download overlap (an upload thread, a download thread, a compute
+ * stream; device output offsets chained on the device). Host arrays may be pageable or pinned
+ * (rp_host_alloc: the copies then run without blocking their threads); pageable destinations
+ * should already be faulted in (first-touch faults cost more than the copy). *total_nnz = exact
+ * nnz; RP_ERR_CAPACITY if it exceeds c_host->capacity (indptr complete, the entries that fit
+ * written) or an RP_I32 indptr cannot hold it. Input indptr monotonicity and column range are
+ * checked on the device (RP_ERR_INVALID). Serialised per projector. */
+int rp_project_stream(rp_projector* h, const rp_csr_in* a_host, int32_t order, int64_t chunk_rows,
+                      const rp_csr_out* c_host, int64_t* total_nnz);
+/* Page-locked host memory (hipHostMalloc) / its release. */
+int rp_host_alloc(int64_t bytes, void** out);
+int rp_host_free(void* p);
 
 /* Synthetic rows on the device: per-row nnz = 1 + Poisson(mean_extra), or exactly -mean_extra
  * when mean_extra < 0 (capped at max_row_nnz),

@@ -24,7 +24,7 @@ EXPORTS = (
     "rp_projector_create_from_device", "rp_projector_destroy", "rp_pack_r_host",
     "rp_project_workspace_bytes", "rp_projector_set_staging", "rp_project_device",
     "rp_project_host_begin", "rp_result_fetch", "rp_result_free", "rp_project",
-    "rp_synth_rows_device", "rp_libsvm_parse_device",
+    "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_project_stream", "rp_host_alloc", "rp_host_free",
 )
 
 
@@ -112,6 +112,9 @@ def load(path: str = None):
         "rp_result_fetch": (ctypes.c_int, [vp, vp, i32, vp, i32, vp]),
         "rp_result_free": (ctypes.c_int, [vp]),
         "rp_project": (ctypes.c_int, [vp, P(CsrIn), i32, ALLOC_FN, vp]),
+        "rp_project_stream": (ctypes.c_int, [vp, P(CsrIn), i32, i64, P(CsrOut), P(i64)]),
+        "rp_host_alloc": (ctypes.c_int, [i64, P(vp)]),
+        "rp_host_free": (ctypes.c_int, [vp]),
         "rp_synth_rows_device": (ctypes.c_int, [ctypes.c_int, i64, i64, dbl, i32, i32, dbl, ctypes.c_uint64,
                                                 vp, i32, vp, vp, vp, P(i64)]),
         "rp_libsvm_parse_device": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, vp, vp, i32, vp, vp, i64, i64, vp,

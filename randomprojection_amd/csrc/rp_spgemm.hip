@@ -27,6 +27,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cmath>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -1774,6 +1775,15 @@ int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, 
         }
         nnz_a = last - first;
     }
+    if (!workspace) {
+        // the projector's own workspace is shared by every caller of this handle (and by the host
+        // path): serialise on the handle and finish the work before releasing it, so no launch on
+        // another stream can reset the look-back header or reallocate the buffer under this one
+        std::lock_guard<std::mutex> lock(h->mu);
+        int rc = project_device_impl(h, a, c, order, nullptr, 0, (hipStream_t)stream, total_nnz, nnz_a);
+        if (rc == RP_OK) HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+        return rc;
+    }
     return project_device_impl(h, a, c, order, workspace, workspace_bytes, (hipStream_t)stream,
                                total_nnz, nnz_a);
 }
@@ -2006,6 +2016,365 @@ int rp_project(rp_projector* h, const rp_csr_in* a, int32_t order, rp_alloc_fn a
     rc = rp_result_fetch(r, ip, ipt, ix, ixt, dx);
     rp_result_free(r);
     return rc;
+}
+
+}  // extern "C"
+
+// ==========================================================================================
+// Chunked host streaming (boundary 2 of SURVEY.md §8(d)): host CSR in -> host CSR out.
+// The recipe projects host-resident partitions (code/clustermode/randomProjection.py:28-54,
+// 107-113); here a host matrix of any size is cut into chunks of rows and three agents overlap:
+//   uploader thread   chunk k+1: indptr/indices/data host -> device slot (hipMemcpyAsync + sync)
+//   calling thread    chunk k:   rebase + input checks, the projection, per-chunk output offsets
+//                                (a device running total, so no host round trip), conversions
+//   downloader thread chunk k-1: indptr (global offsets) and entries device slot -> caller arrays
+// Measured on the box (scripts/probes/pcie_probe2.hip): H2D 55 GB/s and D2H 48-55 GB/s at the
+// same time; a pageable async copy blocks its calling thread for the whole transfer (so each
+// direction gets a thread of its own), pinned ones return at once — both work here, pinned caller
+// buffers (rp_host_alloc) only free the threads earlier. kStreamSlots device slots rotate.
+namespace {
+constexpr int kStreamSlots = 3;
+
+template <typename IP>
+__global__ void stream_rebase_kernel(const IP* __restrict__ raw, int64_t* __restrict__ out, int64_t n1,
+                                     int64_t base0, unsigned long long* __restrict__ bad_row) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n1; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = (int64_t)raw[i];
+        out[i] = v - base0;
+        if (i > 0 && v < (int64_t)raw[i - 1]) atomicMin(bad_row, (unsigned long long)(i - 1));
+    }
+}
+
+// info[0] = this chunk's first output position (running total before it), info[1] = its nnz
+__global__ void stream_finish_kernel(const Workspace* __restrict__ ws, unsigned long long* __restrict__ total,
+                                     unsigned long long* __restrict__ info) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        const unsigned long long b = *total, k = ws->total;
+        info[0] = b;
+        info[1] = k;
+        *total = b + k;
+    }
+}
+
+template <typename OP>
+__global__ void stream_indptr_kernel(const int64_t* __restrict__ cp, OP* __restrict__ out, int64_t n,
+                                     const unsigned long long* __restrict__ info) {
+    const int64_t b = (int64_t)info[0];
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (OP)(cp[i] + b);
+}
+
+struct StreamSlot {
+    DevBuf raw, ap, aj, ax;   // input chunk: indptr as given, rebased int64 indptr, indices, values
+    DevBuf cp, cj, cx;        // output chunk: int64 chunk-relative indptr, int32 indices, values
+    DevBuf optr, oidx;        // download forms: global indptr in the caller's type, int64 indices
+    DevBuf ws, info;          // workspace; info = {base, nnz, first bad column pos, first bad row}
+    int64_t cap = 0;
+    hipEvent_t comp = nullptr;
+};
+
+struct StreamChunk {
+    int64_t r0, rows, e0, nnz;
+};
+
+struct StreamSync {
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t uploaded = 0, launched = 0, downloaded = 0;
+    int err = RP_OK;
+    std::string msg;
+    void set_error(int code) {  // first error wins; the message is this thread's rp_last_error
+        std::lock_guard<std::mutex> l(mu);
+        if (err == RP_OK) {
+            err = code;
+            msg = g_err;
+        }
+        cv.notify_all();
+    }
+    template <typename P>
+    bool wait(P pred) {  // false if an error stopped the pipeline
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return err != RP_OK || pred(); });
+        return err == RP_OK;
+    }
+    void bump(int64_t& ctr) {
+        std::lock_guard<std::mutex> l(mu);
+        ++ctr;
+        cv.notify_all();
+    }
+};
+
+size_t grid_for(int64_t n) { return (size_t)std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 16384); }
+
+int stream_upload(const rp_csr_in* a, const StreamChunk& ck, StreamSlot& s, hipStream_t st, int ips, int vs) {
+    HIP_TRY(hipMemcpyAsync(s.raw.p, (const char*)a->indptr + (size_t)ips * ck.r0, (size_t)ips * (ck.rows + 1),
+                           hipMemcpyHostToDevice, st));
+    if (ck.nnz > 0) {
+        HIP_TRY(hipMemcpyAsync(s.aj.p, a->indices + ck.e0, 4 * (size_t)ck.nnz, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(s.ax.p, (const char*)a->data + (size_t)vs * ck.e0, (size_t)vs * ck.nnz,
+                               hipMemcpyHostToDevice, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return RP_OK;
+}
+
+// the chunk's kernels on the compute stream; output capacity s.cap (the exact nnz lands in info[1])
+int stream_compute(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int order, int ip_type, int vt,
+                   int out_ip, int out_ix, unsigned long long* total, bool last, hipStream_t st) {
+    unsigned long long* info = (unsigned long long*)s.info.p;
+    const unsigned long long init[4] = {0, 0, ~0ull, ~0ull};
+    HIP_TRY(hipMemcpyAsync(info, init, sizeof init, hipMemcpyHostToDevice, st));
+    const int64_t e_base = ck.e0;
+    if (ip_type == RP_I64)
+        hipLaunchKernelGGL((stream_rebase_kernel<int64_t>), dim3(grid_for(ck.rows + 1)), dim3(256), 0, st,
+                           (const int64_t*)s.raw.p, (int64_t*)s.ap.p, ck.rows + 1, e_base, info + 3);
+    else
+        hipLaunchKernelGGL((stream_rebase_kernel<int32_t>), dim3(grid_for(ck.rows + 1)), dim3(256), 0, st,
+                           (const int32_t*)s.raw.p, (int64_t*)s.ap.p, ck.rows + 1, e_base, info + 3);
+    HIP_TRY(hipGetLastError());
+    if (ck.nnz > 0) {
+        hipLaunchKernelGGL(check_columns_kernel, dim3(grid_for(ck.nnz)), dim3(256), 0, st, (const int32_t*)s.aj.p,
+                           ck.nnz, h->m, info + 2);
+        HIP_TRY(hipGetLastError());
+    }
+    rp_csr_in ad{ck.rows, s.ap.p, RP_I64, (const int32_t*)s.aj.p, s.ax.p, vt, ck.nnz};
+    rp_csr_out cd{s.cp.p, RP_I64, s.cj.p, RP_I32, s.cx.p, s.cap};
+    int rc = project_device_impl(h, &ad, &cd, order, s.ws.p, (int64_t)s.ws.bytes, st, nullptr, ck.nnz);
+    if (rc) return rc;
+    hipLaunchKernelGGL(stream_finish_kernel, dim3(1), dim3(64), 0, st, (const Workspace*)s.ws.p, total, info);
+    const int64_t np = ck.rows + (last ? 1 : 0);  // the next chunk writes the shared boundary entry
+    if (out_ip == RP_I64)
+        hipLaunchKernelGGL((stream_indptr_kernel<int64_t>), dim3(grid_for(np)), dim3(256), 0, st,
+                           (const int64_t*)s.cp.p, (int64_t*)s.optr.p, np, (const unsigned long long*)info);
+    else
+        hipLaunchKernelGGL((stream_indptr_kernel<int32_t>), dim3(grid_for(np)), dim3(256), 0, st,
+                           (const int64_t*)s.cp.p, (int32_t*)s.optr.p, np, (const unsigned long long*)info);
+    HIP_TRY(hipGetLastError());
+    if (out_ix == RP_I64 && s.cap > 0) {
+        hipLaunchKernelGGL((convert_kernel<int32_t, int64_t>), dim3(grid_for(s.cap)), dim3(256), 0, st,
+                           (const int32_t*)s.cj.p, (int64_t*)s.oidx.p, s.cap);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(s.comp, st));
+    return RP_OK;
+}
+
+// download chunk results into the caller's arrays; *redo = entries did not fit the device slot
+int stream_download(const StreamChunk& ck, StreamSlot& s, const rp_csr_in* a, const rp_csr_out* c, bool last,
+                    hipStream_t st, int vs, int64_t* nnz_out, bool* redo) {
+    HIP_TRY(hipEventSynchronize(s.comp));
+    unsigned long long info[4];
+    HIP_TRY(hipMemcpyAsync(info, s.info.p, sizeof info, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (info[3] != ~0ull)
+        return fail(RP_ERR_INVALID, "A indptr decreasing at row %lld", (long long)(ck.r0 + (int64_t)info[3]));
+    if (info[2] != ~0ull)
+        return fail(RP_ERR_INVALID, "A column index %d out of range [0, m)", a->indices[ck.e0 + (int64_t)info[2]]);
+    const int64_t base = (int64_t)info[0], k = (int64_t)info[1];
+    *nnz_out = k;
+    const int ops = dtype_size(c->indptr_type), oxs = dtype_size(c->indices_type);
+    const int64_t np = ck.rows + (last ? 1 : 0);
+    HIP_TRY(hipMemcpyAsync((char*)c->indptr + (size_t)ops * ck.r0, s.optr.p, (size_t)ops * np, hipMemcpyDeviceToHost, st));
+    *redo = k > s.cap;
+    const int64_t fit = std::max<int64_t>(0, std::min<int64_t>(k, c->capacity - base));
+    if (!*redo && fit > 0) {
+        const void* src_ix = c->indices_type == RP_I64 ? s.oidx.p : s.cj.p;
+        HIP_TRY(hipMemcpyAsync((char*)c->indices + (size_t)oxs * base, src_ix, (size_t)oxs * fit,
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync((char*)c->data + (size_t)vs * base, s.cx.p, (size_t)vs * fit, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return RP_OK;
+}
+
+int stream_alloc_slot(rp_projector* h, StreamSlot& s, int64_t rows, int64_t nnz, int64_t cap, int ips, int vs,
+                      int out_ip, int out_ix) {
+    const int dev = h->device;
+    int rc;
+    if ((rc = s.raw.ensure((size_t)ips * (rows + 1), dev)) || (rc = s.ap.ensure(8 * (size_t)(rows + 1), dev)) ||
+        (rc = s.aj.ensure(4 * (size_t)std::max<int64_t>(nnz, 1), dev)) ||
+        (rc = s.ax.ensure((size_t)vs * std::max<int64_t>(nnz, 1), dev)) ||
+        (rc = s.cp.ensure(8 * (size_t)(rows + 1), dev)) ||
+        (rc = s.cj.ensure(4 * (size_t)std::max<int64_t>(cap, 1), dev)) ||
+        (rc = s.cx.ensure((size_t)vs * std::max<int64_t>(cap, 1), dev)) ||
+        (rc = s.optr.ensure((size_t)dtype_size(out_ip) * (rows + 1), dev)) ||
+        (rc = s.info.ensure(64, dev)))
+        return rc;
+    if (out_ix == RP_I64 && (rc = s.oidx.ensure(8 * (size_t)std::max<int64_t>(cap, 1), dev))) return rc;
+    const int64_t wsb = rp_project_workspace_bytes(h, rows, nnz);
+    if (wsb < 0) return fail(RP_ERR_INVALID, "workspace size");
+    if ((rc = s.ws.ensure((size_t)wsb, dev))) return rc;
+    s.ws.bytes = (size_t)wsb;
+    s.cap = cap;
+    return RP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_t chunk_rows,
+                      const rp_csr_out* c, int64_t* total_nnz) {
+    if (!h || !a || !c) return fail(RP_ERR_INVALID, "NULL argument");
+    if (order != RP_ORDER_SCIPY && order != RP_ORDER_SORTED) return fail(RP_ERR_INVALID, "bad order");
+    const int ips = dtype_size(a->indptr_type), vs = dtype_size(a->data_type);
+    if (!ips || (a->data_type != RP_F32 && a->data_type != RP_F64)) return fail(RP_ERR_INVALID, "bad A types");
+    if (a->data_type == RP_F32 && h->value_type == RP_F64)
+        return fail(RP_ERR_INVALID, "compute type must be upcast(A, R) = float64 for a float64 R");
+    if ((c->indptr_type != RP_I32 && c->indptr_type != RP_I64) || (c->indices_type != RP_I32 && c->indices_type != RP_I64))
+        return fail(RP_ERR_INVALID, "bad output index types");
+    if (a->n_rows < 0 || !a->indptr || !c->indptr) return fail(RP_ERR_INVALID, "bad CSR arrays");
+    if (c->capacity > 0 && (!c->indices || !c->data)) return fail(RP_ERR_INVALID, "NULL output arrays");
+    const int64_t n = a->n_rows;
+    if (chunk_rows <= 0) chunk_rows = 4 << 20;
+    // chunk plan from indptr at chunk boundaries (the rows inside a chunk are checked on the device)
+    std::vector<StreamChunk> chunks;
+    const int64_t b0 = ptr_at(a->indptr, a->indptr_type, 0);
+    int64_t prev = b0, max_rows = 0, max_nnz = 0;
+    if (b0 < 0) return fail(RP_ERR_INVALID, "A indptr[0] < 0");
+    for (int64_t r = 0; r < n; r += chunk_rows) {
+        const int64_t rows = std::min(chunk_rows, n - r);
+        const int64_t e1 = ptr_at(a->indptr, a->indptr_type, r + rows);
+        if (e1 < prev) return fail(RP_ERR_INVALID, "A indptr decreasing before row %lld", (long long)(r + rows));
+        chunks.push_back({r, rows, prev, e1 - prev});
+        max_rows = std::max(max_rows, rows);
+        max_nnz = std::max(max_nnz, e1 - prev);
+        prev = e1;
+    }
+    if (a->nnz >= 0 && a->nnz < prev - b0) return fail(RP_ERR_INVALID, "A nnz %lld < indptr range %lld",
+                                                      (long long)a->nnz, (long long)(prev - b0));
+    std::lock_guard<std::mutex> lock(h->mu);
+    HIP_TRY(hipSetDevice(h->device));
+    if (chunks.empty()) {
+        if (c->indptr_type == RP_I64) ((int64_t*)c->indptr)[0] = 0; else ((int32_t*)c->indptr)[0] = 0;
+        if (total_nnz) *total_nnz = 0;
+        return RP_OK;
+    }
+    // device output capacity per slot: the expected products of the largest chunk + 6 sigma; a
+    // chunk beyond it is recomputed alone once the pipeline has drained
+    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    const double expect = ppe * (double)max_nnz;
+    const int64_t cap = (int64_t)(1.02 * expect + 8.0 * std::sqrt(expect + 1.0)) + 4096;
+    StreamSlot slots[kStreamSlots];
+    const int ns = (int)std::min<size_t>(kStreamSlots, chunks.size());
+    int rc;
+    for (int i = 0; i < ns; ++i) {
+        if ((rc = stream_alloc_slot(h, slots[i], max_rows, max_nnz, cap, ips, vs, c->indptr_type, c->indices_type)))
+            return rc;
+        HIP_TRY(hipEventCreateWithFlags(&slots[i].comp, hipEventDisableTiming));
+    }
+    DevBuf totbuf;
+    if ((rc = totbuf.ensure(8, h->device))) return rc;
+    hipStream_t st_up = nullptr, st_comp = nullptr, st_down = nullptr;
+    auto cleanup = [&] {
+        for (auto& s : slots)
+            if (s.comp) (void)hipEventDestroy(s.comp);
+        for (hipStream_t s : {st_up, st_comp, st_down})
+            if (s) (void)hipStreamDestroy(s);
+    };
+    if (hipStreamCreateWithFlags(&st_up, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&st_comp, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&st_down, hipStreamNonBlocking) != hipSuccess) {
+        cleanup();
+        return fail(RP_ERR_HIP, "stream creation failed");
+    }
+    if (hipMemsetAsync(totbuf.p, 0, 8, st_comp) != hipSuccess) {
+        cleanup();
+        return fail(RP_ERR_HIP, "memset failed");
+    }
+    const int64_t K = (int64_t)chunks.size();
+    StreamSync sy;
+    std::vector<int64_t> knnz((size_t)K, 0);
+    std::vector<char> redo((size_t)K, 0);
+    const int dev = h->device;
+    std::thread up([&] {
+        if (hipSetDevice(dev) != hipSuccess) return sy.set_error(fail(RP_ERR_HIP, "hipSetDevice"));
+        for (int64_t k = 0; k < K; ++k) {
+            StreamSlot& s = slots[k % ns];
+            // the slot's input is free once chunk k - ns's kernels have run
+            if (!sy.wait([&] { return sy.launched >= k - ns + 1 || k < ns; })) return;
+            if (k >= ns && hipEventSynchronize(s.comp) != hipSuccess)
+                return sy.set_error(fail(RP_ERR_HIP, "event sync (upload)"));
+            if (int r = stream_upload(a, chunks[(size_t)k], s, st_up, ips, vs)) return sy.set_error(r);
+            sy.bump(sy.uploaded);
+        }
+    });
+    std::thread down([&] {
+        if (hipSetDevice(dev) != hipSuccess) return sy.set_error(fail(RP_ERR_HIP, "hipSetDevice"));
+        for (int64_t k = 0; k < K; ++k) {
+            if (!sy.wait([&] { return sy.launched > k; })) return;
+            bool rd = false;
+            if (int r = stream_download(chunks[(size_t)k], slots[k % ns], a, c, k == K - 1, st_down, vs,
+                                        &knnz[(size_t)k], &rd))
+                return sy.set_error(r);
+            redo[(size_t)k] = rd;
+            sy.bump(sy.downloaded);
+        }
+    });
+    for (int64_t k = 0; k < K && sy.err == RP_OK; ++k) {
+        if (!sy.wait([&] { return sy.uploaded > k && sy.downloaded >= k - ns + 1; })) break;
+        if ((rc = stream_compute(h, chunks[(size_t)k], slots[k % ns], order, a->indptr_type, a->data_type,
+                                 c->indptr_type, c->indices_type, (unsigned long long*)totbuf.p, k == K - 1,
+                                 st_comp))) {
+            sy.set_error(rc);
+            break;
+        }
+        sy.bump(sy.launched);
+    }
+    up.join();
+    down.join();
+    if (sy.err != RP_OK) {
+        (void)hipStreamSynchronize(st_comp);
+        cleanup();
+        g_err = sy.msg;
+        return sy.err;
+    }
+    // chunks whose entries exceeded the slot: recompute alone with their exact size
+    int64_t base = 0, total = 0;
+    for (int64_t k = 0; k < K; ++k) total += knnz[(size_t)k];
+    for (int64_t k = 0; k < K && rc == RP_OK; base += knnz[(size_t)k], ++k) {
+        if (!redo[(size_t)k]) continue;
+        StreamSlot& s = slots[0];
+        const StreamChunk& ck = chunks[(size_t)k];
+        if ((rc = stream_alloc_slot(h, s, max_rows, max_nnz, knnz[(size_t)k], ips, vs, c->indptr_type,
+                                    c->indices_type)) ||
+            (rc = stream_upload(a, ck, s, st_up, ips, vs)))
+            break;
+        unsigned long long tot0 = (unsigned long long)base;  // the chunk's base again
+        if (hipMemcpyAsync(totbuf.p, &tot0, 8, hipMemcpyHostToDevice, st_comp) != hipSuccess) {
+            rc = fail(RP_ERR_HIP, "memcpy");
+            break;
+        }
+        if ((rc = stream_compute(h, ck, s, order, a->indptr_type, a->data_type, c->indptr_type, c->indices_type,
+                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp)))
+            break;
+        int64_t kk = 0;
+        bool rd = false;
+        rc = stream_download(ck, s, a, c, k == K - 1, st_down, vs, &kk, &rd);
+        if (rc == RP_OK && (rd || kk != knnz[(size_t)k])) rc = fail(RP_ERR_HIP, "chunk recompute mismatch");
+    }
+    (void)hipStreamSynchronize(st_comp);
+    cleanup();
+    if (rc) return rc;
+    if (total_nnz) *total_nnz = total;
+    if (total > c->capacity)
+        return fail(RP_ERR_CAPACITY, "output capacity %lld < nnz %lld", (long long)c->capacity, (long long)total);
+    if (c->indptr_type == RP_I32 && total > INT32_MAX)
+        return fail(RP_ERR_CAPACITY, "nnz %lld needs an int64 output indptr", (long long)total);
+    return RP_OK;
+}
+
+// pinned (page-locked) host memory for callers that want the stream path's copies fully
+// asynchronous (a data loader filling input chunks, result arrays reused across calls)
+int rp_host_alloc(int64_t bytes, void** out) {
+    if (!out || bytes < 0) return fail(RP_ERR_INVALID, "bad argument");
+    *out = nullptr;
+    HIP_TRY(hipHostMalloc(out, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault));
+    return RP_OK;
+}
+
+int rp_host_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return RP_OK;
 }
 
 int rp_synth_rows_device(int device, int64_t n_rows, int64_t m, double mean_extra,

@@ -38,13 +38,17 @@ def partition_ids(chunk_index: int, n_rows: int) -> np.ndarray:
     return (np.int64(chunk_index) << np.int64(33)) + np.arange(n_rows, dtype=np.int64)
 
 
-def parse_device(text, n_bytes: int, num_features: int, device: int = 0, stream: int = 0, indptr_dtype=None):
+def parse_device(text, n_bytes: int, num_features: int, device: int = 0, stream=None, indptr_dtype=None):
     """Parse libsvm text already in device memory (a uint8 torch tensor, 16-byte aligned).
-    Returns torch tensors (labels f64, indptr, indices i32, data f32) on ``cuda:device``."""
+    Returns torch tensors (labels f64, indptr, indices i32, data f32) on ``cuda:device``. The kernels
+    run on ``stream`` (default: torch's current stream of that device, the stream the tensors are
+    allocated and filled on, so the caching allocator's reuse stays ordered)."""
     import torch
 
     lib = nat.load()
     dev = torch.device("cuda", device)
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
     rows, nnz, err = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(-1)
     tp = ctypes.c_void_p(text.data_ptr())
     nat.check(lib.rp_libsvm_parse_device(device, tp, n_bytes, num_features, None, None, nat.RP_I64, None, None,
@@ -136,10 +140,11 @@ def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order
     import torch
 
     dev = projector.device
+    st = torch.cuda.current_stream(torch.device("cuda", dev)).cuda_stream  # where torch fills/frees the tensors
     for ci, buf in enumerate(iter_chunks(path, chunk_bytes, copy=False)):
         t, n = _to_device(buf, dev)
         del buf  # the view must be gone before the next chunk (the mapping closes at the end)
-        labels, Ap, Aj, Ax = parse_device(t, n, projector.m, dev)
+        labels, Ap, Aj, Ax = parse_device(t, n, projector.m, dev, stream=st)
         del t
         rows = int(labels.numel())
         cap = int(1.3 * Aj.numel() * projector.nnz / max(projector.m, 1)) + 1024
@@ -147,13 +152,13 @@ def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order
         Cj = torch.empty(cap, dtype=torch.int32, device=Cp.device)
         Cx = torch.empty(cap, dtype=torch.float32, device=Cp.device)
         try:
-            k = projector.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=order, nnz_a=int(Aj.numel()))
+            k = projector.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=order, nnz_a=int(Aj.numel()), stream=st)
         except nat.RPError as e:
             if e.code != nat.RP_ERR_CAPACITY:
                 raise
             Cj = torch.empty(e.nnz, dtype=torch.int32, device=Cp.device)
             Cx = torch.empty(e.nnz, dtype=torch.float32, device=Cp.device)
-            k = projector.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=order, nnz_a=int(Aj.numel()))
+            k = projector.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=order, nnz_a=int(Aj.numel()), stream=st)
         if k < 2**31:  # the index dtype scipy's csr_matrix settles on
             Cp = Cp.to(torch.int32)
         C = sp.csr_matrix((_download(Cx[:k]), _download(Cj[:k]), _download(Cp)), shape=(rows, projector.p))

@@ -141,6 +141,14 @@ class Projector:
         if indices.dtype != np.int32 and indices.size and (indices.min() < 0 or indices.max() >= self.m):
             raise ValueError("column index out of range")
         n = len(indptr) - 1
+        if indptr.ndim != 1 or n < 0:
+            raise ValueError("index pointer should be a 1-D array of at least one entry")
+        if n >= 0 and (int(indptr[0]) < 0 or int(indptr[-1]) < int(indptr[0])):
+            raise ValueError("index pointer values must start at a non-negative value and be non-decreasing")
+        if aj.ndim != 1 or data.ndim != 1 or aj.size < int(indptr[-1]) or data.size < int(indptr[-1]):
+            # scipy's check_format: "indices and data should have the same size" / "Last value of
+            # index pointer should be less than the size of index and data arrays"
+            raise ValueError("Last value of index pointer should be less than the size of index and data arrays")
         a = nat.CsrIn(n, nat.ptr(indptr).value, nat.idx_code(indptr.dtype), nat.ptr(aj).value,
                       nat.ptr(data).value, nat.val_code(T), int(indptr[-1] - indptr[0]) if n >= 0 else 0)
         code = nat.RP_ORDER_SORTED if order == "sorted" else nat.RP_ORDER_SCIPY

@@ -28,6 +28,16 @@ from .srp_matrix import check_density, johnson_lindenstrauss_min_dim, sparse_ran
 __all__ = ["SparseRandomProjection", "johnson_lindenstrauss_min_dim"]
 
 
+def _fingerprint(comp, n_sample: int = 4096):
+    arrs = [comp.data, comp.indices, comp.indptr] if sp.issparse(comp) else [np.asarray(comp).ravel()]
+    fp = [comp.shape, str(comp.dtype)]
+    for a in arrs:
+        a = np.asarray(a)
+        step = max(1, a.size // n_sample)
+        fp.append((a.__array_interface__["data"][0], a.size, a[::step].tobytes()))
+    return tuple(fp)
+
+
 class SparseRandomProjection(_SkSparseRandomProjection):
     """``sklearn.random_projection.SparseRandomProjection`` with a GPU ``transform``.
 
@@ -47,15 +57,23 @@ class SparseRandomProjection(_SkSparseRandomProjection):
         return sparse_random_matrix(n_components, n_features, density=self.density_,
                                     random_state=random_state)
 
+    def fit(self, X, y=None):
+        self.__dict__.pop("_rp_cache", None)  # a refit always re-uploads R
+        return super().fit(X, y)
+
     def _projector(self) -> Projector:
+        """The resident R for the current ``components_``. The cache holds the matrix object itself
+        (compared by identity, so a freed-and-reused ``id`` can never alias an older matrix) and a
+        fingerprint of its buffers: data pointers, sizes and a strided sample of the values and
+        indices, which catches in-place edits of the fitted matrix in the common cases."""
         comp = self.components_
-        key = (id(comp), getattr(comp, "nnz", None), comp.shape, str(comp.dtype))
+        fp = _fingerprint(comp)
         cached = getattr(self, "_rp_cache", None)
-        if cached is None or cached[0] != key:
+        if cached is None or cached[0] is not comp or cached[1] != fp:
             R = comp.T if sp.issparse(comp) else sp.csr_matrix(np.asarray(comp).T)
-            cached = (key, Projector(R, device=self.device))
+            cached = (comp, fp, Projector(R, device=self.device))
             self._rp_cache = cached
-        return cached[1]
+        return cached[2]
 
     def transform(self, X):
         check_is_fitted(self)

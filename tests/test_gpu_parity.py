@@ -156,6 +156,30 @@ def test_sklearn_transform_bitwise(dtype, container):
     assert same_bits(ours.transform(X), ref.transform(X))
 
 
+def test_sklearn_refit_and_inplace_edit_reupload():
+    """fit, transform, refit (other seed), transform: the second transform uses the new matrix
+    (the cached GPU copy of R is keyed by the matrix object itself, never by a reusable id);
+    an in-place edit of components_ is picked up as well."""
+    from sklearn.random_projection import SparseRandomProjection as SkSRP
+    from randomprojection_amd import SparseRandomProjection
+
+    rng = np.random.default_rng(2)
+    X = kdd_like(rng, 2000, 20_000, values="normal")
+    ours = SparseRandomProjection(n_components=256, random_state=1).fit(X)
+    Y1 = ours.transform(X)
+    for seed in (2, 3, 1):
+        ours.set_params(random_state=seed).fit(X)
+        ref = SkSRP(n_components=256, random_state=seed).fit(X)
+        Yr = ref.transform(X)
+        Y = ours.transform(X)
+        assert_same_csr(Y, Yr.indptr, Yr.indices, Yr.data)
+        if seed != 1:
+            assert (Y != Y1).nnz > 0
+    ours.components_.data[:] = -ours.components_.data   # in place: same object, new values
+    Y = ours.transform(X)
+    assert same_bits(Y.data, -Y1.data) and np.array_equal(Y.indices, Y1.indices)
+
+
 @pytest.mark.parametrize("powerlaw", [False, True])
 @pytest.mark.parametrize("layout", ["auto", "generic"])
 def test_random_kdd_shape_vs_oracle(powerlaw, layout):
