@@ -2119,7 +2119,8 @@ int stream_upload(const rp_csr_in* a, const StreamChunk& ck, StreamSlot& s, hipS
 }
 
 // the chunk's kernels on the compute stream; output capacity s.cap (the exact nnz lands in info[1])
-int stream_compute(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int order, int ip_type, int vt,
+int stream_compute(rp_projector* h, const rp_csr_in* a, const StreamChunk& ck, StreamSlot& s, int order,
+                   int ip_type, int vt,
                    int out_ip, int out_ix, unsigned long long* total, bool last, hipStream_t st) {
     unsigned long long* info = (unsigned long long*)s.info.p;
     const unsigned long long init[4] = {0, 0, ~0ull, ~0ull};
@@ -2137,6 +2138,16 @@ int stream_compute(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int or
                            ck.nnz, h->m, info + 2);
         HIP_TRY(hipGetLastError());
     }
+    // a decreasing indptr or a column outside [0, m) would send the kernels out of bounds: check
+    // before projecting (a short wait on this stream only; the copy threads keep going)
+    unsigned long long chk[4];
+    HIP_TRY(hipMemcpyAsync(chk, info, sizeof chk, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (chk[3] != ~0ull)
+        return fail(RP_ERR_INVALID, "A indptr decreasing at row %lld", (long long)(ck.r0 + (int64_t)chk[3]));
+    if (chk[2] != ~0ull)
+        return fail(RP_ERR_INVALID, "A column index %d out of range [0, %lld)", a->indices[ck.e0 + (int64_t)chk[2]],
+                    (long long)h->m);
     rp_csr_in ad{ck.rows, s.ap.p, RP_I64, (const int32_t*)s.aj.p, s.ax.p, vt, ck.nnz};
     rp_csr_out cd{s.cp.p, RP_I64, s.cj.p, RP_I32, s.cx.p, s.cap};
     int rc = project_device_impl(h, &ad, &cd, order, s.ws.p, (int64_t)s.ws.bytes, st, nullptr, ck.nnz);
@@ -2166,10 +2177,6 @@ int stream_download(const StreamChunk& ck, StreamSlot& s, const rp_csr_in* a, co
     unsigned long long info[4];
     HIP_TRY(hipMemcpyAsync(info, s.info.p, sizeof info, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (info[3] != ~0ull)
-        return fail(RP_ERR_INVALID, "A indptr decreasing at row %lld", (long long)(ck.r0 + (int64_t)info[3]));
-    if (info[2] != ~0ull)
-        return fail(RP_ERR_INVALID, "A column index %d out of range [0, m)", a->indices[ck.e0 + (int64_t)info[2]]);
     const int64_t base = (int64_t)info[0], k = (int64_t)info[1];
     *nnz_out = k;
     const int ops = dtype_size(c->indptr_type), oxs = dtype_size(c->indices_type);
@@ -2312,7 +2319,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
     });
     for (int64_t k = 0; k < K && sy.err == RP_OK; ++k) {
         if (!sy.wait([&] { return sy.uploaded > k && sy.downloaded >= k - ns + 1; })) break;
-        if ((rc = stream_compute(h, chunks[(size_t)k], slots[k % ns], order, a->indptr_type, a->data_type,
+        if ((rc = stream_compute(h, a, chunks[(size_t)k], slots[k % ns], order, a->indptr_type, a->data_type,
                                  c->indptr_type, c->indices_type, (unsigned long long*)totbuf.p, k == K - 1,
                                  st_comp))) {
             sy.set_error(rc);
@@ -2344,7 +2351,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
             rc = fail(RP_ERR_HIP, "memcpy");
             break;
         }
-        if ((rc = stream_compute(h, ck, s, order, a->indptr_type, a->data_type, c->indptr_type, c->indices_type,
+        if ((rc = stream_compute(h, a, ck, s, order, a->indptr_type, a->data_type, c->indptr_type, c->indices_type,
                                  (unsigned long long*)totbuf.p, k == K - 1, st_comp)))
             break;
         int64_t kk = 0;

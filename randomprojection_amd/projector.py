@@ -27,6 +27,8 @@ from . import hostmem
 __all__ = ["Projector", "get_projector", "scipy_result_index_dtype"]
 
 _INT32_MAX = np.iinfo(np.int32).max
+# host matrices from this many rows go through the chunked stream path (rp_project_stream)
+STREAM_MIN_ROWS = 8 << 20
 
 
 def _operand_csr(R) -> sp.csr_matrix:
@@ -141,6 +143,9 @@ class Projector:
         if indices.dtype != np.int32 and indices.size and (indices.min() < 0 or indices.max() >= self.m):
             raise ValueError("column index out of range")
         n = len(indptr) - 1
+        if n >= STREAM_MIN_ROWS:  # large host matrices: chunked, overlapped upload/compute/download
+            return self.project_stream(indptr, aj, data, order=order, out_index_dtype=out_index_dtype,
+                                       _index_rule_arrays=(indptr, indices))
         if indptr.ndim != 1 or n < 0:
             raise ValueError("index pointer should be a 1-D array of at least one entry")
         if n >= 0 and (int(indptr[0]) < 0 or int(indptr[-1]) < int(indptr[0])):
@@ -183,6 +188,69 @@ class Projector:
             raise ValueError(self._lib.rp_last_error().decode())
         nat.check(rc)
         return out["Cp"], out["Cj"], out["Cx"]
+
+    def project_stream(self, indptr, indices, data, order: str = "scipy", chunk_rows: int = 0, out=None,
+                       out_index_dtype=None, _index_rule_arrays=None):
+        """Host CSR in -> host CSR out through ``rp_project_stream``: rows in chunks (default 4M)
+        whose upload, projection and download overlap (boundary 2, BASELINE configs[1]'s chunked
+        row streaming). ``out``: optional ``(indptr, indices, data)`` host arrays to fill (reused
+        buffers avoid first-touch page faults; capacity = len(indices)); else recycled host memory
+        sized from the expected nnz, with one exact retry if that was short. Returns
+        ``(indptr, indices[:nnz], data[:nnz])``."""
+        indptr = np.ascontiguousarray(indptr)
+        if indptr.dtype not in (np.int32, np.int64):
+            indptr = indptr.astype(np.int64)
+        indices = np.asarray(indices)
+        T = self.compute_dtype(np.asarray(data).dtype)
+        data = np.ascontiguousarray(data, dtype=T)
+        aj = np.ascontiguousarray(indices, dtype=np.int32)
+        n = len(indptr) - 1
+        if indptr.ndim != 1 or n < 0:
+            raise ValueError("index pointer should be a 1-D array of at least one entry")
+        nnz_a = int(indptr[-1]) - int(indptr[0])
+        if int(indptr[0]) < 0 or nnz_a < 0 or aj.size < int(indptr[-1]) or data.size < int(indptr[-1]):
+            raise ValueError("Last value of index pointer should be less than the size of index and data arrays")
+        rule = _index_rule_arrays if _index_rule_arrays is not None else (indptr, indices)
+
+        def alloc(cap, dt):
+            dt = np.dtype(dt)
+            return hostmem.empty(n + 1, dt), hostmem.empty(max(cap, 1), dt), hostmem.empty(max(cap, 1), T)
+
+        keep_dt = None if out is None else np.dtype(out[0].dtype)  # a caller's out fixes the index dtype
+        if out is None:
+            exp = nnz_a * self.nnz / max(self.m, 1)
+            cap = int(1.02 * exp + 8.0 * np.sqrt(exp + 1.0)) + 65536
+            dt = out_index_dtype or (np.int64 if self.r_index_dtype == np.int64 else scipy_result_index_dtype(rule, cap))
+            out = alloc(cap, dt)
+        Cp, Cj, Cx = out
+        a = nat.CsrIn(n, nat.ptr(indptr).value, nat.idx_code(indptr.dtype), nat.ptr(aj).value,
+                      nat.ptr(data).value, nat.val_code(T), nnz_a)
+        code = nat.RP_ORDER_SORTED if order == "sorted" else nat.RP_ORDER_SCIPY
+        total = ctypes.c_int64(0)
+        for attempt in range(2):
+            if Cx.dtype != T or Cj.dtype != Cp.dtype or Cp.size != n + 1:
+                raise ValueError("out arrays: indptr of n_rows + 1 entries, indices of indptr's dtype, data of "
+                                 f"the compute dtype {T}")
+            c = nat.CsrOut(nat.ptr(Cp).value, nat.idx_code(Cp.dtype), nat.ptr(Cj).value, nat.idx_code(Cj.dtype),
+                           nat.ptr(Cx).value, int(Cj.size))
+            with self._lock:
+                rc = self._lib.rp_project_stream(self._h, ctypes.byref(a), code, int(chunk_rows), ctypes.byref(c),
+                                                 ctypes.byref(total))
+            k = int(total.value)
+            if rc == nat.RP_ERR_CAPACITY and attempt == 0:
+                dt = keep_dt or out_index_dtype or (np.int64 if self.r_index_dtype == np.int64
+                                                    else scipy_result_index_dtype(rule, k))
+                Cp, Cj, Cx = alloc(k, dt)
+                continue
+            if rc == nat.RP_ERR_INVALID:
+                raise ValueError(self._lib.rp_last_error().decode())
+            nat.check(rc)
+            break
+        if keep_dt is None and out_index_dtype is None and Cp.dtype == np.int64 and self.r_index_dtype != np.int64:
+            want = scipy_result_index_dtype(rule, k)   # the estimate passed 2^31, the result did not
+            if want != Cp.dtype:
+                Cp, Cj = Cp.astype(want), Cj[:k].astype(want)
+        return Cp, Cj[:k], Cx[:k]
 
     def matmul(self, A, order: str = "scipy"):
         """``A @ R`` for sparse A, returning what scipy returns (container of A's class)."""

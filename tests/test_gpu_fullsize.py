@@ -77,6 +77,15 @@ def test_configs1_full_size(kdd, dist):
         assert 5.3 < nnz / KDD_ROWS < 6.3
         check_csr_on_device(Cp, Cj, nnz, sm.KDD_P, sorted_rows=(order == "sorted"))
         assert check_rows_vs_oracle(rows, Ap, Aj, Ax, Cp, Cj, Cx, R, order=order) > 350_000
+        if dist == "uniform" and order == "scipy":
+            # the same rows as a host CSR through the chunked stream path (boundary 2): the whole
+            # 119.7M-row result equals the device-resident one, every byte
+            ip, ix, dx = P.project_stream(Ap.cpu().numpy(), Aj.cpu().numpy(), Ax.cpu().numpy())
+            assert ix.size == nnz
+            assert np.array_equal(ip, Cp.cpu().numpy())
+            assert np.array_equal(ix, Cj[:nnz].cpu().numpy())
+            assert np.array_equal(dx.view(np.uint32), Cx[:nnz].cpu().numpy().view(np.uint32))
+            del ip, ix, dx
         del Cp, Cj, Cx
         torch.cuda.empty_cache()
 
