@@ -814,18 +814,18 @@ stage_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj
         if (e < n) {
             const uint32_t pos = s_hist[(uint32_t)jj[i] >> sb] + rk[i];
             s_key[pos] = (e << 20) | ((uint32_t)jj[i] & mask);
-            s_val[pos] = Axt[e];
+            if (SX) s_val[pos] = Axt[e];
         }
     }
     __syncthreads();
     uint32_t* __restrict__ St = S + (ea - a0);
-    T* __restrict__ SXt = SX + (ea - a0);
+    T* __restrict__ SXt = SX ? SX + (ea - a0) : nullptr;
 #pragma unroll
     for (int i = 0; i < kMaxE; ++i) {
         const uint32_t e = tid + i * kBlock;
         if (e < n) {
             St[e] = s_key[e];
-            SXt[e] = s_val[e];
+            if (SX) SXt[e] = s_val[e];
         }
     }
 }
@@ -931,6 +931,486 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
             ws->total = G + cnt;
         }
         __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Row-lane pipeline (packed R, short rows — KDD2012: 11 entries, 6 products/row).
+// No look-back and no waiting: every wave's output goes to a fixed slot, then one scan and one copy.
+//   lpr_main_kernel   one workgroup per tile of 256 rows, one wave per 64 rows. The tile's R
+//                     descriptors (gathered from W directly, or the staged W32 words of
+//                     stage_partition/stage_gather) land in LDS by entry; then each wave runs ONE
+//                     flat pass over its entries (64 consecutive entries per step, no divergence):
+//                     row of an entry from a row-start bitmap (popcount), its products, their kept
+//                     prefix (wave scan) = their place in the wave's slot in first-touch order, and
+//                     per row a product count and a 3 x 64-bit column signature (LDS atomics).
+//                     A row whose signature cannot rule out a repeated column (~0.5% real repeats,
+//                     ~1% false alarms) is recomputed by its lane exactly (LDS scratch: leaders sum
+//                     their column group in sequence order) into the same slot range.
+//   lpr_heavy_*       tiles beyond a cap (entries, side table, scratch, slot): the exact dense
+//                     accumulator (heavy_tile) counts, then writes them in place.
+//   lpr_scan_kernel   exclusive scan of the per-wave counts (decoupled look-back, 4096 per block)
+//   lpr_copy_kernel   slots -> C: each row reversed (scipy's reverse first-touch order) or as is
+//                     (ascending, sorted in the slot), indptr from the per-row counts.
+// Per-row semantics are scipy's csr_matmat exactly: first touch = product order, sums start at +0
+// and add in product order, sum != 0 kept.
+constexpr int kLprRows = 256;      // rows per tile (4 waves x 64 rows)
+constexpr int kLprSide = 128;      // 64-bit W words of features with > 2 R entries, per tile
+constexpr int kLprFlagWords = kCapAMax / 64 + 1;  // row-start bitmap words per wave
+
+struct LprSpace {
+    uint32_t* cnt;        // 4 x n_tiles: kept entries of each wave (slot fill)
+    unsigned long long* off;  // 4 x n_tiles: exclusive prefix of cnt (+ base)
+    uint32_t* hlist;      // heavy tiles, count in ws->n_deferred
+    uint32_t* tflag;      // n_tiles: 1 = heavy (lpr_heavy_write places the tile)
+    uint32_t* rowmeta;    // n_tiles x 256: row's first slot position << 16 | row's entry count
+    uint16_t* cols;       // 4 x n_tiles x slot
+    unsigned char* vals;  // 4 x n_tiles x slot x sizeof(T)
+    unsigned long long* scan_state;  // one per 4096-wave scan block
+    uint32_t slot;        // kept-entry capacity of one wave
+};
+
+__device__ __forceinline__ uint32_t lpr_h2(uint32_t col) { return (col * 0x9E3779B1u) >> 26; }
+
+// products of an entry with LDS descriptor d: bits 30-31 = n <= 2 inline 15-bit slots (sign << 14 |
+// col) in R's storage order; n = 3: the W word in side[d & mask] (<= 4 inline, or an O record)
+__device__ __forceinline__ uint32_t lpr_count(uint32_t d, const uint64_t* side, const uint16_t* O) {
+    const uint32_t n = d >> 30;
+    if (n < 3) return n;
+    const uint64_t w = side[d & 0x3fffffffu];
+    const uint32_t nw = (uint32_t)(w >> 61);
+    return nw != 7 ? nw : O[w & kLow61];
+}
+// t-th product's (sign << 14 | col)
+__device__ __forceinline__ uint32_t lpr_slot(uint32_t d, uint32_t t, const uint64_t* side, const uint16_t* O) {
+    if ((d >> 30) < 3) return (d >> (15 * t)) & 0x7fffu;
+    const uint64_t w = side[d & 0x3fffffffu];
+    if ((w >> 61) != 7) return (uint32_t)(w >> (15 * t)) & 0x7fffu;
+    const uint32_t e = O[(w & kLow61) + 1 + t];
+    return ((e & 0x8000u) >> 1) | (e & 0x3fffu);
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl_scan_t(T v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const T t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// inclusive wave scan with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15/31)
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
+template <typename T, typename IP, bool STAGED>
+__global__ void __launch_bounds__(kLprRows)
+lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                const T* __restrict__ Ax, const uint32_t* __restrict__ S, const uint32_t* __restrict__ D,
+                int cap_a, unsigned n_tiles, int order, LprSpace sp, Workspace* ws) {
+    extern __shared__ __align__(16) unsigned char lds[];          // s_desc[cap_a] u32
+    __shared__ uint16_t s_rowptr[kLprRows + 1];
+    __shared__ uint64_t s_side[kLprSide];
+    __shared__ uint64_t s_flag[4][kLprFlagWords];                  // row-start bitmap per wave
+    __shared__ uint64_t s_sig[4][64][3];                            // column signatures; exact-path scratch after
+    __shared__ uint64_t s_susp[4];                                  // rows flagged for the exact path
+    __shared__ uint16_t s_kst[4][64];
+    __shared__ uint8_t s_nz2row[4][64];
+    __shared__ uint32_t s_nside, s_scr[4];
+    __shared__ int s_bad;
+    uint32_t* s_desc = reinterpret_cast<uint32_t*>(lds);
+
+    const unsigned tile = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int64_t row0 = (int64_t)tile * kLprRows;
+    const int nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
+    const int64_t ea = (int64_t)Ap[row0];
+    const int64_t ne64 = (int64_t)Ap[row0 + nrows] - ea;
+    if (tid == 0) {
+        s_nside = 0;
+        s_bad = ne64 > cap_a;
+    }
+    if (tid < 4) s_scr[tid] = 0;
+    __syncthreads();
+    auto go_heavy = [&]() {  // one lane of the tile: the heavy path takes the whole tile
+        if (atomicOr(&sp.tflag[tile], 1u) == 0u) sp.hlist[atomicAdd(&ws->n_deferred, 1u)] = tile;
+    };
+    if (s_bad) {  // uniform: too many entries for the tile's LDS
+        if (tid == 0) go_heavy();
+        return;
+    }
+    STAMP(0);
+    const uint32_t ne = (uint32_t)ne64;
+    for (int r = tid; r <= nrows; r += kLprRows) s_rowptr[r] = (uint16_t)((int64_t)Ap[row0 + r] - ea);
+    // ---- step A: R descriptors of the tile's entries into LDS, by entry
+    auto put_desc = [&](uint32_t e, uint64_t w) {  // w: a W word (n <= 2 fits the 32-bit form)
+        const uint32_t n = (uint32_t)(w >> 61);
+        uint32_t d = (n << 30) | (uint32_t)(w & 0x3fffffffu);
+        if (n > 2) {
+            const uint32_t k = atomicAdd(&s_nside, 1u);
+            if (k < (uint32_t)kLprSide) s_side[k] = w;
+            else s_bad = 1;
+            d = 0xc0000000u | k;
+        }
+        s_desc[e] = d;
+    };
+    constexpr int kU = 12;  // loads of a round issued before any is used
+    if constexpr (STAGED) {
+        const int64_t qb = ea - (int64_t)Ap[0];
+        const uint32_t* __restrict__ St = S + qb;
+        const uint32_t* __restrict__ Dt = D + qb;
+        for (uint32_t q0 = tid; q0 < ne; q0 += kU * kLprRows) {
+            uint32_t sv[kU], dv[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint32_t q = q0 + u * kLprRows;
+                sv[u] = q < ne ? St[q] : 0u;
+                dv[u] = q < ne ? Dt[q] : 0u;
+            }
+            uint64_t wv[kU];  // code 3: the full W word of a feature with > 2 entries
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                wv[u] = (q0 + u * kLprRows < ne && (dv[u] >> 30) == 3) ? R.W[dv[u] & 0x3fffffffu] : 0ull;
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (q0 + u * kLprRows < ne) {
+                    if ((dv[u] >> 30) == 3) put_desc(sv[u] >> 20, wv[u]);
+                    else s_desc[sv[u] >> 20] = dv[u];  // the W32 word: same bits as W's slots 0-1
+                }
+        }
+    } else {
+        const int32_t* __restrict__ Ajt = Aj + ea;
+        for (uint32_t q0 = tid; q0 < ne; q0 += kU * kLprRows) {
+            int32_t jv[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint32_t e = q0 + u * kLprRows;
+                jv[u] = e < ne ? Ajt[e] : -1;
+            }
+            uint64_t w[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) w[u] = jv[u] >= 0 ? R.W[jv[u]] : 0ull;
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (q0 + u * kLprRows < ne) put_desc(q0 + u * kLprRows, w[u]);
+        }
+    }
+    STAMP(1);
+    __syncthreads();
+    STAMP(2);
+    if (s_bad) {  // uniform: side table full
+        if (tid == 0) go_heavy();
+        return;
+    }
+    // ---- step B: one wave per 64 rows, one flat pass over the wave's entries
+    const int w = tid >> 6, lane = tid & 63;
+    const int r = tid;  // this lane's row (for per-row work)
+    const bool valid = r < nrows;
+    const uint32_t rs = valid ? s_rowptr[r] : 0u, re = valid ? s_rowptr[r + 1] : 0u;
+    const int rlast = std::min(64 * w + 64, nrows);
+    const uint32_t E0 = s_rowptr[std::min(64 * w, nrows)], E1 = s_rowptr[rlast];
+    const uint32_t nsteps = (E1 - E0 + 63) >> 6;
+    for (uint32_t k = lane; k < nsteps; k += 64) s_flag[w][k] = 0ull;
+    s_sig[w][lane][0] = s_sig[w][lane][1] = s_sig[w][lane][2] = 0ull;
+    if (lane == 0) s_susp[w] = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    const bool nonempty = re > rs;
+    const uint64_t ne_mask = __ballot(nonempty);
+    if (nonempty) {
+        const uint32_t b = rs - E0;
+        atomicOr(reinterpret_cast<unsigned long long*>(&s_flag[w][b >> 6]), 1ull << (b & 63));
+        s_nz2row[w][__builtin_popcountll(ne_mask & ((1ull << lane) - 1))] = (uint8_t)lane;
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint16_t* __restrict__ oc = sp.cols + ((size_t)tile * 4 + w) * sp.slot;
+    T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + ((size_t)tile * 4 + w) * sp.slot;
+    uint32_t carry_r = 0, carry_k = 0;
+    const T* __restrict__ Axw = Ax + ea;
+    auto step = [&](uint32_t j, T x) {
+        const uint32_t e = E0 + 64 * j + lane;
+        const bool ve = e < E1;
+        const uint64_t fw = s_flag[w][j];
+        const uint32_t nr = carry_r + (uint32_t)__builtin_popcountll(fw & ((2ull << lane) - 1)) - 1u;
+        const uint32_t row = ve ? s_nz2row[w][nr] : 0u;
+        const uint32_t d = ve ? s_desc[e] : 0u;
+        const uint32_t np = ve ? lpr_count(d, s_side, R.O) : 0u;
+        const bool nzx = tmul<T>(x, mag) != T(0);  // all products of an entry share |x * mag|
+        const uint32_t kc = nzx ? np : 0u;
+        const uint32_t kinc = wave_scan_dpp(kc);
+        const uint32_t K = carry_k + kinc - kc;
+        if (ve && ((fw >> lane) & 1ull)) s_kst[w][row] = (uint16_t)K;  // the row's first entry
+        if (np) {
+            // products in place (first-touch order) and a Bloom test per product against the
+            // row's earlier products: 3 x 64-bit filters, a product whose 3 bits were all set
+            // already flags its row for the exact path (every real repeat does)
+            uint64_t g0 = 0, g1 = 0, g2 = 0;
+            for (uint32_t t = 0; t < np; ++t) {
+                const uint32_t sl = lpr_slot(d, t, s_side, R.O);
+                const uint32_t col = sl & 0x3fffu;
+                g0 |= 1ull << (col & 63);
+                g1 |= 1ull << ((col >> 6) & 63);
+                g2 |= 1ull << lpr_h2(col);
+                if (kc && K + t < sp.slot) {
+                    oc[K + t] = (uint16_t)col;
+                    ov[K + t] = tadd<T>(T(0), tmul<T>(x, (sl & 0x4000u) ? -mag : mag));
+                }
+            }
+            const uint64_t o0 = atomicOr(reinterpret_cast<unsigned long long*>(&s_sig[w][row][0]), g0);
+            const uint64_t o1 = atomicOr(reinterpret_cast<unsigned long long*>(&s_sig[w][row][1]), g1);
+            const uint64_t o2 = atomicOr(reinterpret_cast<unsigned long long*>(&s_sig[w][row][2]), g2);
+            bool hit = false;
+            for (uint32_t t = 0; t < np && !hit; ++t) {
+                const uint32_t col = lpr_slot(d, t, s_side, R.O) & 0x3fffu;
+                hit = ((o0 >> (col & 63)) & (o1 >> ((col >> 6) & 63)) & (o2 >> lpr_h2(col)) & 1ull) != 0;
+            }
+            if (hit) atomicOr(reinterpret_cast<unsigned long long*>(&s_susp[w]), 1ull << row);
+        }
+        carry_k += __builtin_amdgcn_readlane(kinc, 63);
+        carry_r += (uint32_t)__builtin_popcountll(fw);
+        };
+    // values straight from HBM in entry order (coalesced), four steps in flight ahead of use
+    auto ldx = [&](uint32_t j) { const uint32_t e = E0 + 64 * j + lane; return e < E1 ? Axw[e] : T(0); };
+    T x0 = ldx(0), x1 = ldx(1), x2 = ldx(2), x3 = ldx(3);
+    for (uint32_t j = 0; j < nsteps; j += 4) {
+        T c0 = x0, c1 = x1, c2 = x2, c3 = x3;
+        x0 = ldx(j + 4);
+        x1 = ldx(j + 5);
+        x2 = ldx(j + 6);
+        x3 = ldx(j + 7);
+        step(j, c0);
+        if (j + 1 < nsteps) step(j + 1, c1);
+        if (j + 2 < nsteps) step(j + 2, c2);
+        if (j + 3 < nsteps) step(j + 3, c3);
+    }
+    bool overflow = carry_k > sp.slot;
+    __builtin_amdgcn_wave_barrier();
+    STAMP(3);
+    // ---- per row: kept count; flagged rows are redone exactly
+    const uint32_t kst = nonempty ? s_kst[w][lane] : 0u;
+    const uint64_t after = ne_mask & ~((2ull << lane) - 1);  // the next non-empty row ends this one
+    const int nxt = after ? __builtin_ctzll(after) : 64;
+    const uint32_t kst_next = __shfl(kst, nxt & 63, 64);
+    const uint32_t kend = nxt < 64 ? kst_next : carry_k;
+    uint32_t kept = nonempty ? kend - kst : 0u;
+    uint64_t todo = s_susp[w];
+    __builtin_amdgcn_wave_barrier();  // signatures are dead from here: the scratch reuses them
+    constexpr int kScr = (int)((64 * 3 * 8 - 16) / (2 + sizeof(T)));
+    uint16_t* scol = reinterpret_cast<uint16_t*>(&s_sig[w][0][0]);
+    T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(&s_sig[w][0][0]) + ((2 * kScr + 15) & ~15));
+    if (__ballot(overflow)) todo = 0;
+    // exact path, one flagged row at a time, the whole wave on it: its products in sequence order
+    // into the scratch, then every product checks for an earlier one of its column (first touch);
+    // a leader sums its group in order; kept leaders land in the row's slot range in that order
+    while (todo) {
+        const int R0 = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint32_t a0 = __shfl(rs, R0, 64), a1 = __shfl(re, R0, 64), kR = __shfl(kst, R0, 64);
+        uint32_t nprod = 0;
+        for (uint32_t e0 = a0; e0 < a1; e0 += 64) {
+            const uint32_t e = e0 + lane;
+            const bool in = e < a1;
+            const uint32_t d = in ? s_desc[e] : 0u;
+            const T x = in ? Axw[e] : T(0);
+            const uint32_t np = in ? lpr_count(d, s_side, R.O) : 0u;
+            const uint32_t inc = wave_scan_dpp(np);
+            const uint32_t q0 = nprod + inc - np;
+            for (uint32_t t = 0; t < np; ++t)
+                if (q0 + t < (uint32_t)kScr) {
+                    const uint32_t sl = lpr_slot(d, t, s_side, R.O);
+                    scol[q0 + t] = (uint16_t)(sl & 0x3fffu);
+                    sval[q0 + t] = tmul<T>(x, (sl & 0x4000u) ? -mag : mag);
+                }
+            nprod += __builtin_amdgcn_readlane(inc, 63);
+        }
+        if (nprod > (uint32_t)kScr) {
+            overflow = true;
+            break;
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t nk = 0;
+        for (uint32_t q0 = 0; q0 < nprod; q0 += 64) {
+            const uint32_t q = q0 + lane;
+            bool lead = q < nprod;
+            T sum = T(0);
+            if (lead) {
+                const uint16_t cq = scol[q];
+                for (uint32_t b = 0; b < q && lead; ++b) lead = scol[b] != cq;
+                if (lead) {
+                    sum = tadd<T>(T(0), sval[q]);
+                    for (uint32_t b = q + 1; b < nprod; ++b)
+                        if (scol[b] == cq) sum = tadd<T>(sum, sval[b]);
+                }
+            }
+            const bool keep = lead && sum != T(0);
+            const uint32_t ki = wave_scan_dpp(keep ? 1u : 0u);
+            if (keep) {
+                oc[kR + nk + ki - 1] = scol[q];
+                ov[kR + nk + ki - 1] = sum;
+            }
+            nk += __builtin_amdgcn_readlane(ki, 63);
+        }
+        if (lane == R0) kept = nk;
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (__ballot(overflow)) {  // this wave cannot finish on the fast path: the whole tile goes heavy
+        if (lane == 0) go_heavy();
+        return;
+    }
+    if (order == RP_ORDER_SORTED && kept > 1) {  // ascending columns inside the row's slot range
+        for (uint32_t a = kst + 1; a < kst + kept; ++a) {
+            const uint16_t kc = oc[a];
+            const T kv = ov[a];
+            uint32_t b = a;
+            while (b > kst && oc[b - 1] > kc) {
+                oc[b] = oc[b - 1];
+                ov[b] = ov[b - 1];
+                --b;
+            }
+            oc[b] = kc;
+            ov[b] = kv;
+        }
+    }
+    if (valid) sp.rowmeta[(size_t)tile * kLprRows + r] = (kst << 16) | kept;
+    const uint32_t wtot = __builtin_amdgcn_readlane(wave_scan_dpp(valid ? kept : 0u), 63);
+    if (lane == 0) sp.cnt[(size_t)tile * 4 + w] = wtot;
+    STAMP(4);
+    STAMP(5);
+    STAMP(6);
+}
+
+// heavy tiles, pass 0: the exact dense accumulator counts their rows (grid-stride over the list);
+// the count goes to the tile's first wave slot, the other three are zeroed
+template <typename T, typename IP>
+__global__ void __launch_bounds__(kBlock)
+lpr_heavy_count_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                       const T* __restrict__ Ax, int p, LprSpace sp, Workspace* ws) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    const unsigned nh = ws->n_deferred;
+    uint32_t* s_rowc = reinterpret_cast<uint32_t*>(lds + heavy_lds_bytes(p, sizeof(T)) - 4 * kBlock);
+    for (unsigned i = blockIdx.x; i < nh; i += gridDim.x) {
+        const unsigned tile = sp.hlist[i];
+        const int64_t row0 = (int64_t)tile * kLprRows;
+        const int nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
+        heavy_tile<T, IP, int64_t, int32_t, PackedR>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 0, 0,
+                                                     nullptr, nullptr, nullptr, false, RP_ORDER_SCIPY);
+        uint32_t tot;
+        (void)block_excl_scan(threadIdx.x < (unsigned)nrows ? s_rowc[threadIdx.x] : 0u, s_wsum, &tot);
+        if (threadIdx.x < 4) sp.cnt[(size_t)tile * 4 + threadIdx.x] = threadIdx.x == 0 ? tot : 0u;
+        __syncthreads();
+    }
+}
+
+// heavy tiles, pass 1: write at the tile's offset (after the scan)
+template <typename T, typename IP, typename OP, typename OI>
+__global__ void __launch_bounds__(kBlock)
+lpr_heavy_write_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                       const T* __restrict__ Ax, int p, LprSpace sp, Workspace* ws, OP* __restrict__ Cp,
+                       OI* __restrict__ Cj, T* __restrict__ Cx, unsigned long long capacity, int order) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    const unsigned nh = ws->n_deferred;
+    const unsigned n_tiles = (unsigned)((n_rows + kLprRows - 1) / kLprRows);
+    uint32_t* s_rowc = reinterpret_cast<uint32_t*>(lds + heavy_lds_bytes(p, sizeof(T)) - 4 * kBlock);
+    for (unsigned i = blockIdx.x; i < nh; i += gridDim.x) {
+        const unsigned tile = sp.hlist[i];
+        const int64_t row0 = (int64_t)tile * kLprRows;
+        const int nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
+        const unsigned long long G = sp.off[(size_t)tile * 4];
+        const uint32_t cnt = sp.cnt[(size_t)tile * 4];
+        heavy_tile<T, IP, OP, OI, PackedR>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 1, G, Cp, Cj, Cx,
+                                           G + cnt <= capacity, order);
+        if (tile == n_tiles - 1 && threadIdx.x == 0) Cp[n_rows] = (OP)(G + cnt);
+        __syncthreads();
+    }
+}
+
+// exclusive scan of the wave counts: 4096 per block (16 per thread), decoupled look-back over
+// blocks (taken in order from a ticket so every predecessor is running or done)
+constexpr int kScanPer = 16;
+__global__ void __launch_bounds__(kBlock)
+lpr_scan_kernel(LprSpace sp, size_t n, unsigned long long base, Workspace* ws, unsigned* ticket) {
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    __shared__ unsigned s_blk;
+    __shared__ unsigned long long s_off;
+    if (threadIdx.x == 0) s_blk = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const unsigned blk = s_blk;
+    const size_t t0 = (size_t)blk * (kBlock * kScanPer) + (size_t)threadIdx.x * kScanPer;
+    uint32_t v[kScanPer];
+    uint32_t local = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        v[i] = t0 + i < n ? sp.cnt[t0 + i] : 0u;
+        local += v[i];
+    }
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(local, s_wsum, &tot);
+    if (threadIdx.x < 64) {
+        const unsigned long long g = lookback_wave(sp.scan_state, blk, tot, ws);
+        if (threadIdx.x == 0) s_off = g + base;
+    }
+    __syncthreads();
+    unsigned long long o = s_off + ex;
+#pragma unroll
+    for (int i = 0; i < kScanPer; ++i) {
+        if (t0 + i < n) sp.off[t0 + i] = o;
+        o += v[i];
+    }
+    if (t0 < n && t0 + kScanPer >= n) ws->total = o - base;  // the thread holding the last count
+}
+
+// slots -> C: one workgroup per tile (grid-stride), one wave per 64-row slot; rows reversed for
+// scipy's order (the slot holds first-touch order) or copied as they are (sorted in the slot)
+template <typename T, typename OP, typename OI>
+__global__ void __launch_bounds__(kBlock)
+lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ Cp, OI* __restrict__ Cj,
+                T* __restrict__ Cx, unsigned long long capacity, int order) {
+    const T* vals = reinterpret_cast<const T*>(sp.vals);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (unsigned tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        if (sp.tflag[tile]) continue;  // lpr_heavy_write_kernel places it
+        const size_t wt = (size_t)tile * 4 + w;
+        const unsigned long long G = sp.off[wt];
+        const uint32_t cnt = sp.cnt[wt];
+        const int64_t row0 = (int64_t)tile * kLprRows;
+        const int nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
+        const int r = 64 * w + lane;
+        const uint32_t meta = r < nrows ? sp.rowmeta[(size_t)tile * kLprRows + r] : 0u;
+        const uint32_t c = meta & 0xffffu, src = meta >> 16;
+        const uint32_t inc = wave_incl_scan_t<uint32_t>(c, lane);
+        const uint32_t pre = inc - c;
+        if (r < nrows) Cp[row0 + r] = (OP)(G + pre);
+        if (tile == n_tiles - 1 && threadIdx.x == kBlock - 1) Cp[n_rows] = (OP)(G + cnt);
+        if (G + cnt > capacity) continue;
+        const uint16_t* sc = sp.cols + wt * sp.slot;
+        const T* sv = vals + wt * sp.slot;
+        for (uint32_t o0 = 0; o0 < cnt; o0 += 64) {  // uniform trip count: every lane takes part in the shuffles
+            const uint32_t o = o0 + lane;
+            // the row holding output o: the last lane whose prefix is <= o (binary search)
+            int lo = 0;
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1) {
+                const uint32_t pv = __shfl(pre, lo + step, 64);
+                if (lo + step < 64 && pv <= o) lo += step;
+            }
+            // several empty rows share a prefix: the row that owns o is the last of them with c > 0
+            const uint32_t rp = __shfl(pre, lo, 64), rc = __shfl(c, lo, 64), rsrc = __shfl(src, lo, 64);
+            const uint32_t i = o - rp;
+            if (o < cnt) {
+                const uint32_t s = order == RP_ORDER_SORTED ? rsrc + i : rsrc + rc - 1 - i;
+                Cj[G + o] = (OI)sc[s];
+                Cx[G + o] = sv[s];
+            }
+        }
     }
 }
 
@@ -1151,6 +1631,11 @@ struct Plan {
            d = 0, sx = 0;
     unsigned long long pool_cap = 0;
     size_t total = 0;
+    // row-lane pipeline (lpr_*): tiles of kLprRows rows, every tile's output in a fixed slot
+    bool lpr = false;
+    uint32_t lpr_slot = 0;
+    int64_t scan_blocks = 0;
+    size_t lcnt = 0, loff = 0, lhl = 0, ltf = 0, lrow = 0, lcols = 0, lvals = 0;
 };
 
 constexpr unsigned kDeferCopyGrid = 32768;  // copy workgroups (grid-stride over the deferred list)
@@ -1161,13 +1646,74 @@ constexpr bool kStageAuto = false;              // auto picks staging (off until
 constexpr int64_t kStageMinNnz = 1 << 22;      // auto: stage only launches this large
 constexpr int64_t kStageMinTable = 64ll << 20;  // ... and only a W past L2/MALL-friendly sizes
 
+// Row-lane pipeline choice: packed R, short rows (one lane walks a row), few products per row.
+// RP_PIPE=tile|lpr forces a pipeline where it can run (tests, measurements).
+constexpr double kLprMaxRowEntries = 24.0, kLprMaxRowProducts = 24.0;
+constexpr bool kLprAuto = false;       // auto picks the row-lane pipeline (off until it measures faster)
+constexpr bool kLprStageAuto = false;  // ... and staging inside it
+bool lpr_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
+    if (h->layout != RP_LAYOUT_PACKED || n_rows <= 0 || nnz_a < 0) return false;
+    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    const double avg = (double)nnz_a / (double)n_rows;
+    const bool fits = avg <= kLprMaxRowEntries && avg * ppe <= kLprMaxRowProducts &&
+                      avg * kLprRows + 6.0 * std::sqrt(avg * kLprRows) + 40.0 <= kCapAMax;
+    const char* e = getenv("RP_PIPE");
+    if (e && !strcmp(e, "tile")) return false;
+    if (e && !strcmp(e, "lpr")) return fits;
+    return kLprAuto && fits;
+}
+
 Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_stage = true,
                int vs = 8, bool allow_defer = true) {
     Plan pl;
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
+    if (lpr_wanted(h, n_rows, nnz_a) && allow_defer) {
+        // one lane per row: 256-row tiles, entries capped for LDS (6 sigma), the output slot for the
+        // expected products + 7.5 sigma (a tile beyond either takes the exact heavy path)
+        pl.lpr = true;
+        const double avg = (double)nnz_a / (double)n_rows;
+        const double ents = avg * kLprRows, prods = std::max(1.0, ents * ppe);
+        pl.caps.rpt = kLprRows;
+        pl.caps.cap_a = (int)std::min<double>(kCapAMax, ((int)(ents + 6.0 * std::sqrt(ents) + 40.0) + 63) & ~63);
+        pl.caps.cap_p = (int)std::min<double>(65535.0, ((int)(prods + 9.5 * std::sqrt(prods) + 64.0) + 63) & ~63);
+        const double prods_w = std::max(1.0, avg * 64 * ppe);  // one wave's slot: 64 rows
+        pl.lpr_slot = (uint32_t)std::min<double>(65535.0, ((int)(prods_w + 12.0 * std::sqrt(prods_w) + 64.0) + 63) & ~63);
+        pl.n_tiles = (n_rows + kLprRows - 1) / kLprRows;
+        const size_t nw = 4 * (size_t)pl.n_tiles;
+        pl.scan_blocks = ((int64_t)nw + kBlock * kScanPer - 1) / (kBlock * kScanPer);
+        // header, scan states and the per-tile heavy flags are zeroed by one memset per call
+        pl.ltf = al(sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(pl.scan_blocks, 1));
+        pl.head = pl.ltf + al(4 * (size_t)pl.n_tiles);
+        pl.lcnt = pl.head;
+        pl.loff = pl.lcnt + al(4 * nw);
+        pl.lhl = pl.loff + al(8 * nw);
+        pl.lrow = pl.lhl + al(4 * (size_t)pl.n_tiles);
+        pl.lcols = pl.lrow + al(4 * (size_t)kLprRows * (size_t)pl.n_tiles);
+        pl.lvals = pl.lcols + al(2 * (size_t)pl.lpr_slot * nw);
+        pl.total = pl.lvals + al((size_t)vs * (size_t)pl.lpr_slot * nw);
+        const bool want_stage = h->stage_mode == 1 || (h->stage_mode == -1 && kLprStageAuto &&
+                                                       nnz_a >= kStageMinNnz && 8 * h->m >= kStageMinTable);
+        if (allow_stage && want_stage && h->W32.p) {
+            int sb = h->stage_sb > 0 ? h->stage_sb : 19;
+            auto nbk = [&](int b) { return (int)((h->m + ((int64_t)1 << b) - 1) >> b); };
+            while (h->stage_sb <= 0 && nbk(sb) > kStageMaxNB && sb < 20) ++sb;
+            if (sb >= 1 && sb <= 20 && nbk(sb) <= kStageMaxNB) {
+                pl.staged = true;
+                pl.sb = sb;
+                pl.nb = std::max(nbk(sb), 1);
+                pl.ostride = (uint32_t)((pl.n_tiles + 31) & ~int64_t(31));
+                pl.te = pl.total;
+                pl.offt = pl.te + al(8 * (size_t)pl.n_tiles);
+                pl.s = pl.offt + al(2 * (size_t)(pl.nb + 1) * pl.ostride);
+                pl.d = pl.s + al(4 * (size_t)nnz_a);
+                pl.total = pl.d + al(4 * (size_t)nnz_a);
+            }
+        }
+        return pl;
+    }
     pl.caps = choose_caps(n_rows, nnz_a >= 0 ? nnz_a : n_rows * 11, ppe);
     pl.n_tiles = n_rows > 0 ? (n_rows + pl.caps.rpt - 1) / pl.caps.rpt : 0;
-    auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
     pl.head = al(sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(pl.n_tiles, 1));
     pl.total = pl.head;
     if (pl.n_tiles > 0 && allow_defer && nnz_a >= 0) {  // deferred-output list, headers, pool
@@ -1261,11 +1807,83 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
     return RP_OK;
 }
 
+size_t lpr_lds_bytes(int cap_a, size_t) { return (4 * (size_t)cap_a + 15) & ~size_t(15); }
+
+template <typename T, typename IP, typename OP, typename OI>
+int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
+               Workspace* ws, const Plan& pl, hipStream_t st) {
+    char* base = reinterpret_cast<char*>(ws);
+    LprSpace sp{reinterpret_cast<uint32_t*>(base + pl.lcnt), reinterpret_cast<unsigned long long*>(base + pl.loff),
+                reinterpret_cast<uint32_t*>(base + pl.lhl), reinterpret_cast<uint32_t*>(base + pl.ltf),
+                reinterpret_cast<uint32_t*>(base + pl.lrow), reinterpret_cast<uint16_t*>(base + pl.lcols),
+                reinterpret_cast<unsigned char*>(base + pl.lvals), reinterpret_cast<unsigned long long*>(ws + 1),
+                pl.lpr_slot};
+    const unsigned n_tiles = (unsigned)pl.n_tiles;
+    const IP* Ap = (const IP*)a->indptr;
+    const T* Ax = (const T*)a->data;
+    const uint32_t *S = nullptr, *D = nullptr;
+    if (pl.staged) {
+        int64_t* TE = reinterpret_cast<int64_t*>(base + pl.te);
+        uint16_t* OFFT = reinterpret_cast<uint16_t*>(base + pl.offt);
+        uint32_t* Sw = reinterpret_cast<uint32_t*>(base + pl.s);
+        uint32_t* Dw = reinterpret_cast<uint32_t*>(base + pl.d);
+        const size_t plds = 4 * (size_t)pl.caps.cap_a;
+        HIP_TRY(hipFuncSetAttribute((const void*)stage_partition_kernel<T, IP>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(plds + sizeof(T) * pl.caps.cap_a)));
+        hipLaunchKernelGGL((stage_partition_kernel<T, IP>), dim3(n_tiles), dim3(kBlock), plds + sizeof(T) * pl.caps.cap_a,
+                           st, Ap, a->indices, Ax, a->n_rows, pl.caps, n_tiles, pl.sb, pl.nb, pl.ostride, Sw,
+                           (T*)nullptr, OFFT, TE);
+        HIP_TRY(hipGetLastError());
+        const unsigned groups = (n_tiles + kStageTB - 1) / kStageTB;
+        const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * groups;
+        hipLaunchKernelGGL(stage_gather_kernel, dim3(grid), dim3(kBlock), kStageMap, st, (const uint32_t*)h->W32.p,
+                           (const int64_t*)TE, n_tiles, pl.sb, pl.nb, pl.ostride, groups, (const uint16_t*)OFFT,
+                           (const uint32_t*)Sw, Dw);
+        HIP_TRY(hipGetLastError());
+        S = Sw;
+        D = Dw;
+    }
+    const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T));
+    if (pl.staged) {
+        HIP_TRY(hipFuncSetAttribute((const void*)lpr_main_kernel<T, IP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+        hipLaunchKernelGGL((lpr_main_kernel<T, IP, true>), dim3(n_tiles), dim3(kLprRows), lds, st, R, mag, a->n_rows,
+                           Ap, a->indices, Ax, S, D, pl.caps.cap_a, n_tiles, order, sp, ws);
+    } else {
+        HIP_TRY(hipFuncSetAttribute((const void*)lpr_main_kernel<T, IP, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+        hipLaunchKernelGGL((lpr_main_kernel<T, IP, false>), dim3(n_tiles), dim3(kLprRows), lds, st, R, mag, a->n_rows,
+                           Ap, a->indices, Ax, S, D, pl.caps.cap_a, n_tiles, order, sp, ws);
+    }
+    HIP_TRY(hipGetLastError());
+    const size_t hl = heavy_lds_bytes(h->p, sizeof(T));
+    HIP_TRY(hipFuncSetAttribute((const void*)lpr_heavy_count_kernel<T, IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)hl));
+    hipLaunchKernelGGL((lpr_heavy_count_kernel<T, IP>), dim3(256), dim3(kBlock), hl, st, R, mag, a->n_rows, Ap,
+                       a->indices, Ax, (int)h->p, sp, ws);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(lpr_scan_kernel, dim3((unsigned)pl.scan_blocks), dim3(kBlock), 0, st, sp, 4 * (size_t)n_tiles,
+                       0ull, ws, &ws->tile_counter);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL((lpr_copy_kernel<T, OP, OI>), dim3(std::min<unsigned>(n_tiles, 1u << 20)), dim3(kBlock), 0, st,
+                       sp, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices, (T*)c->data,
+                       (unsigned long long)c->capacity, order);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFuncSetAttribute((const void*)lpr_heavy_write_kernel<T, IP, OP, OI>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl));
+    hipLaunchKernelGGL((lpr_heavy_write_kernel<T, IP, OP, OI>), dim3(256), dim3(kBlock), hl, st, R, mag, a->n_rows, Ap,
+                       a->indices, Ax, (int)h->p, sp, ws, (OP*)c->indptr, (OI*)c->indices, (T*)c->data,
+                       (unsigned long long)c->capacity, order);
+    HIP_TRY(hipGetLastError());
+    return RP_OK;
+}
+
 template <typename T, typename IP, typename OP, typename OI, typename RL>
 int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
                  int order, Workspace* ws, unsigned n_tiles, const Plan& pl, size_t lds,
                  hipStream_t st) {
     if constexpr (std::is_same<RL, PackedR>::value) {
+        if (pl.lpr) return launch_lpr<T, IP, OP, OI>(R, mag, h, a, c, order, ws, pl, st);
         if (pl.staged) {
             char* base = reinterpret_cast<char*>(ws);
             int64_t* TE = reinterpret_cast<int64_t*>(base + pl.te);
@@ -1360,7 +1978,8 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
             plan = make_plan(h, a->n_rows, nnz_a_hint, false, vs, false);
     }
     const Caps& caps = plan.caps;
-    const size_t lds = lds_bytes_for(caps, dtype_size(a->data_type), h->p);
+    const size_t lds = plan.lpr ? std::max(lpr_lds_bytes(caps.cap_a, (size_t)vs), heavy_lds_bytes(h->p, (size_t)vs))
+                                : lds_bytes_for(caps, dtype_size(a->data_type), h->p);
     if (lds > 160 * 1024 - 4096)
         return fail(RP_ERR_UNSUPPORTED, "p=%lld too large for the LDS accumulator (%zu bytes)",
                     (long long)h->p, lds);
