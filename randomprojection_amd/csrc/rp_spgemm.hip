@@ -1020,13 +1020,13 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     __shared__ uint16_t s_rowptr[kLprRows + 1];
     __shared__ uint64_t s_side[kLprSide];
     __shared__ uint64_t s_flag[4][kLprFlagWords];                  // row-start bitmap per wave
-    __shared__ uint64_t s_sig[4][64][3];                            // column signatures; exact-path scratch after
     __shared__ uint64_t s_susp[4];                                  // rows flagged for the exact path
     __shared__ uint16_t s_kst[4][64];
     __shared__ uint8_t s_nz2row[4][64];
     __shared__ uint32_t s_nside, s_scr[4];
     __shared__ int s_bad;
     uint32_t* s_desc = reinterpret_cast<uint32_t*>(lds);
+    uint16_t* s_colbuf = reinterpret_cast<uint16_t*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)));  // 4 x slot
 
     const unsigned tile = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1119,7 +1119,6 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     const uint32_t E0 = s_rowptr[std::min(64 * w, nrows)], E1 = s_rowptr[rlast];
     const uint32_t nsteps = (E1 - E0 + 63) >> 6;
     for (uint32_t k = lane; k < nsteps; k += 64) s_flag[w][k] = 0ull;
-    s_sig[w][lane][0] = s_sig[w][lane][1] = s_sig[w][lane][2] = 0ull;
     if (lane == 0) s_susp[w] = 0ull;
     __builtin_amdgcn_wave_barrier();
     const bool nonempty = re > rs;
@@ -1132,50 +1131,50 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     __builtin_amdgcn_wave_barrier();
     uint16_t* __restrict__ oc = sp.cols + ((size_t)tile * 4 + w) * sp.slot;
     T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + ((size_t)tile * 4 + w) * sp.slot;
-    uint32_t carry_r = 0, carry_k = 0;
+    uint16_t* cb = s_colbuf + (size_t)w * sp.slot;  // the wave's kept columns, slot order
     const T* __restrict__ Axw = Ax + ea;
+    uint32_t carry_r = 0, carry_k = 0;
+    const T nmag = -mag;
     auto step = [&](uint32_t j, T x) {
         const uint32_t e = E0 + 64 * j + lane;
         const bool ve = e < E1;
         const uint64_t fw = s_flag[w][j];
         const uint32_t nr = carry_r + (uint32_t)__builtin_popcountll(fw & ((2ull << lane) - 1)) - 1u;
-        const uint32_t row = ve ? s_nz2row[w][nr] : 0u;
+        const uint32_t row = s_nz2row[w][nr & 63];
         const uint32_t d = ve ? s_desc[e] : 0u;
-        const uint32_t np = ve ? lpr_count(d, s_side, R.O) : 0u;
+        const uint32_t n = d >> 30;
+        const uint32_t np = n < 3 ? n : lpr_count(d, s_side, R.O);  // n == 3: a side entry (rare)
         const bool nzx = tmul<T>(x, mag) != T(0);  // all products of an entry share |x * mag|
         const uint32_t kc = nzx ? np : 0u;
         const uint32_t kinc = wave_scan_dpp(kc);
         const uint32_t K = carry_k + kinc - kc;
         if (ve && ((fw >> lane) & 1ull)) s_kst[w][row] = (uint16_t)K;  // the row's first entry
-        if (np) {
-            // products in place (first-touch order) and a Bloom test per product against the
-            // row's earlier products: 3 x 64-bit filters, a product whose 3 bits were all set
-            // already flags its row for the exact path (every real repeat does)
-            uint64_t g0 = 0, g1 = 0, g2 = 0;
-            for (uint32_t t = 0; t < np; ++t) {
-                const uint32_t sl = lpr_slot(d, t, s_side, R.O);
-                const uint32_t col = sl & 0x3fffu;
-                g0 |= 1ull << (col & 63);
-                g1 |= 1ull << ((col >> 6) & 63);
-                g2 |= 1ull << lpr_h2(col);
-                if (kc && K + t < sp.slot) {
-                    oc[K + t] = (uint16_t)col;
-                    ov[K + t] = tadd<T>(T(0), tmul<T>(x, (sl & 0x4000u) ? -mag : mag));
-                }
-            }
-            const uint64_t o0 = atomicOr(reinterpret_cast<unsigned long long*>(&s_sig[w][row][0]), g0);
-            const uint64_t o1 = atomicOr(reinterpret_cast<unsigned long long*>(&s_sig[w][row][1]), g1);
-            const uint64_t o2 = atomicOr(reinterpret_cast<unsigned long long*>(&s_sig[w][row][2]), g2);
-            bool hit = false;
-            for (uint32_t t = 0; t < np && !hit; ++t) {
-                const uint32_t col = lpr_slot(d, t, s_side, R.O) & 0x3fffu;
-                hit = ((o0 >> (col & 63)) & (o1 >> ((col >> 6) & 63)) & (o2 >> lpr_h2(col)) & 1ull) != 0;
-            }
-            if (hit) atomicOr(reinterpret_cast<unsigned long long*>(&s_susp[w]), 1ull << row);
+        const uint32_t sl0 = d & 0x7fffu, sl1 = (d >> 15) & 0x7fffu;
+        if (n < 3 && kc >= 1 && K < sp.slot) {
+            oc[K] = (uint16_t)(sl0 & 0x3fffu);
+            ov[K] = tadd<T>(T(0), tmul<T>(x, (sl0 & 0x4000u) ? nmag : mag));
+            cb[K] = (uint16_t)(sl0 & 0x3fffu);
         }
+        if (n < 3 && kc >= 2 && K + 1 < sp.slot) {
+            oc[K + 1] = (uint16_t)(sl1 & 0x3fffu);
+            ov[K + 1] = tadd<T>(T(0), tmul<T>(x, (sl1 & 0x4000u) ? nmag : mag));
+            cb[K + 1] = (uint16_t)(sl1 & 0x3fffu);
+        }
+        if (__ballot(n == 3 && kc > 0)) {  // side entries: every product in R's storage order
+            if (n == 3 && kc > 0)
+                for (uint32_t t = 0; t < np && K + t < sp.slot; ++t) {
+                    const uint32_t sl = lpr_slot(d, t, s_side, R.O);
+                    oc[K + t] = (uint16_t)(sl & 0x3fffu);
+                    ov[K + t] = tadd<T>(T(0), tmul<T>(x, (sl & 0x4000u) ? nmag : mag));
+                    cb[K + t] = (uint16_t)(sl & 0x3fffu);
+                }
+        }
+        // a zero product (x == 0, or underflow) is not in the slot: its row takes the exact path,
+        // which sees every product
+        if (ve && np > 0 && !nzx) atomicOr(reinterpret_cast<unsigned long long*>(&s_susp[w]), 1ull << row);
         carry_k += __builtin_amdgcn_readlane(kinc, 63);
         carry_r += (uint32_t)__builtin_popcountll(fw);
-        };
+    };
     // values straight from HBM in entry order (coalesced), four steps in flight ahead of use
     auto ldx = [&](uint32_t j) { const uint32_t e = E0 + 64 * j + lane; return e < E1 ? Axw[e] : T(0); };
     T x0 = ldx(0), x1 = ldx(1), x2 = ldx(2), x3 = ldx(3);
@@ -1193,18 +1192,32 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     bool overflow = carry_k > sp.slot;
     __builtin_amdgcn_wave_barrier();
     STAMP(3);
-    // ---- per row: kept count; flagged rows are redone exactly
+    // ---- per row: kept count and a Bloom check of its columns (3 x 64-bit filters in registers):
+    // a column whose 3 bits are all set already flags the row for the exact path (every real
+    // repeat does; false alarms ~ (i/64)^3 for the i-th product)
     const uint32_t kst = nonempty ? s_kst[w][lane] : 0u;
     const uint64_t after = ne_mask & ~((2ull << lane) - 1);  // the next non-empty row ends this one
     const int nxt = after ? __builtin_ctzll(after) : 64;
     const uint32_t kst_next = __shfl(kst, nxt & 63, 64);
     const uint32_t kend = nxt < 64 ? kst_next : carry_k;
     uint32_t kept = nonempty ? kend - kst : 0u;
-    uint64_t todo = s_susp[w];
-    __builtin_amdgcn_wave_barrier();  // signatures are dead from here: the scratch reuses them
-    constexpr int kScr = (int)((64 * 3 * 8 - 16) / (2 + sizeof(T)));
-    uint16_t* scol = reinterpret_cast<uint16_t*>(&s_sig[w][0][0]);
-    T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(&s_sig[w][0][0]) + ((2 * kScr + 15) & ~15));
+    bool hit = false;
+    if (!overflow) {
+        uint64_t b0 = 0, b1 = 0, b2 = 0;
+        for (uint32_t q = kst; q < kend; ++q) {
+            const uint32_t col = cb[q];
+            const uint64_t m0 = 1ull << (col & 63), m1 = 1ull << ((col >> 6) & 63), m2 = 1ull << lpr_h2(col);
+            hit |= (b0 & m0) && (b1 & m1) && (b2 & m2);
+            b0 |= m0;
+            b1 |= m1;
+            b2 |= m2;
+        }
+    }
+    uint64_t todo = s_susp[w] | __ballot(hit);  // lane == row within the wave
+    __builtin_amdgcn_wave_barrier();  // the column buffer is dead from here: the scratch reuses it
+    const int kScr = (int)((sp.slot * 2 - 16) / (2 + sizeof(T)));
+    uint16_t* scol = cb;
+    T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(cb) + ((2 * (size_t)kScr + 15) & ~size_t(15)));
     if (__ballot(overflow)) todo = 0;
     // exact path, one flagged row at a time, the whole wave on it: its products in sequence order
     // into the scratch, then every product checks for an earlier one of its column (first touch);
@@ -1252,14 +1265,20 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             const bool keep = lead && sum != T(0);
             const uint32_t ki = wave_scan_dpp(keep ? 1u : 0u);
             if (keep) {
-                oc[kR + nk + ki - 1] = scol[q];
-                ov[kR + nk + ki - 1] = sum;
+                if (kR + nk + ki - 1 >= sp.slot) overflow = true;
+                else {
+                    oc[kR + nk + ki - 1] = scol[q];
+                    ov[kR + nk + ki - 1] = sum;
+                }
             }
             nk += __builtin_amdgcn_readlane(ki, 63);
         }
         if (lane == R0) kept = nk;
         __builtin_amdgcn_wave_barrier();
     }
+    // a row that gained entries in the exact path (its side entries were not in the slot) must
+    // still end before the next row's range
+    if (kst + kept > kend && nonempty) overflow = true;
     if (__ballot(overflow)) {  // this wave cannot finish on the fast path: the whole tile goes heavy
         if (lane == 0) go_heavy();
         return;
@@ -1807,7 +1826,9 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
     return RP_OK;
 }
 
-size_t lpr_lds_bytes(int cap_a, size_t) { return (4 * (size_t)cap_a + 15) & ~size_t(15); }
+size_t lpr_lds_bytes(int cap_a, size_t, uint32_t slot) {
+    return ((4 * (size_t)cap_a + 15) & ~size_t(15)) + 4 * 2 * (size_t)slot;
+}
 
 template <typename T, typename IP, typename OP, typename OI>
 int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
@@ -1843,7 +1864,7 @@ int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, con
         S = Sw;
         D = Dw;
     }
-    const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T));
+    const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot);
     if (pl.staged) {
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_main_kernel<T, IP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
@@ -1978,7 +1999,7 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
             plan = make_plan(h, a->n_rows, nnz_a_hint, false, vs, false);
     }
     const Caps& caps = plan.caps;
-    const size_t lds = plan.lpr ? std::max(lpr_lds_bytes(caps.cap_a, (size_t)vs), heavy_lds_bytes(h->p, (size_t)vs))
+    const size_t lds = plan.lpr ? std::max(lpr_lds_bytes(caps.cap_a, (size_t)vs, plan.lpr_slot), heavy_lds_bytes(h->p, (size_t)vs))
                                 : lds_bytes_for(caps, dtype_size(a->data_type), h->p);
     if (lds > 160 * 1024 - 4096)
         return fail(RP_ERR_UNSUPPORTED, "p=%lld too large for the LDS accumulator (%zu bytes)",
