@@ -113,6 +113,7 @@ struct PackedR {
     const uint16_t* O;
 };
 constexpr uint64_t kOvf = 7ull << 61;
+constexpr uint32_t kW32J = (1u << 26) - 1;  // feature index bits of a code-3 W32 word (m <= 2^26)
 constexpr uint64_t kLow61 = (1ull << 61) - 1;
 // Generic CSR (any values): Bp int32 (m + 1), Bj uint16, Bx in the compute type.
 template <typename T>
@@ -534,7 +535,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     eixp[i >> 1] |= ei << (16 * (i & 1));
                     dw[i] = w;
                     cnt = w >> 30;
-                    if (cnt == 3) (void)r_describe<T>(R, (int32_t)(w & 0x3fffffffu), cnt);
+                    if (cnt == 3) (void)r_describe<T>(R, (int32_t)(w & kW32J), cnt);
                 } else {
                     x[i] = Axt[e];
                     d[i] = r_describe<T>(R, Ajt[e], cnt);
@@ -567,7 +568,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                         e = (eixp[i >> 1] >> (16 * (i & 1))) & 0xffffu;
                         const uint32_t code = dw[i] >> 30;
                         uint32_t cnt;
-                        de = code == 3 ? r_describe<T>(R, (int32_t)(dw[i] & 0x3fffffffu), cnt)
+                        de = code == 3 ? r_describe<T>(R, (int32_t)(dw[i] & kW32J), cnt)
                                        : (((uint64_t)code << 61) | (uint64_t)(dw[i] & 0x3fffffffu));
                     } else {
                         e = tid + i * kBlock;
@@ -748,12 +749,28 @@ constexpr int kStageTB = 256;     // tiles per gather workgroup (one per thread 
 constexpr int kStageMaxNB = 256;  // buckets (one per thread in the partition scan)
 constexpr int kStageMap = 16384;  // gather: element -> run map entries (u8) in LDS
 
-__global__ void build_w32_kernel(const uint64_t* __restrict__ W, uint32_t* __restrict__ W32, int64_t m) {
+// bit j of BM = feature j has at least one R entry (57% of KDD2012 features have none)
+__global__ void build_bitmap_kernel(const uint64_t* __restrict__ W, uint32_t* __restrict__ BM, int64_t m) {
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < (m + 31) / 32;
+         k += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t b = 0;
+        for (int i = 0; i < 32 && k * 32 + i < m; ++i) b |= (W[k * 32 + i] >> 61) ? (1u << i) : 0u;
+        BM[k] = b;
+    }
+}
+
+// W32 word of a feature with more than 2 R entries: code 3, its entry count (4 bits, 15 = "15 or
+// more") and j (26 bits: staging needs m <= 2^26), so the row-lane kernel knows every entry's
+// product count without the dependent W gather
+__global__ void build_w32_kernel(const uint64_t* __restrict__ W, const uint16_t* __restrict__ O,
+                                 uint32_t* __restrict__ W32, int64_t m) {
     for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m;
          j += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t w = W[j];
         const uint32_t n = (uint32_t)(w >> 61);
-        W32[j] = n <= 2 ? ((n << 30) | (uint32_t)(w & 0x3fffffffu)) : (0xc0000000u | (uint32_t)j);
+        const uint32_t cnt = n != 7 ? n : O[w & kLow61];
+        W32[j] = n <= 2 ? ((n << 30) | (uint32_t)(w & 0x3fffffffu))
+                        : (0xc0000000u | (std::min(cnt, 15u) << 26) | (uint32_t)j);
     }
 }
 
@@ -895,6 +912,63 @@ stage_gather_kernel(const uint32_t* __restrict__ W32, const int64_t* __restrict_
     }
 }
 
+// Filtered staged gather for the row-lane pipeline. Workgroup (bucket b, tile group g) on XCD b % 8
+// (round-robin dispatch: workgroup i runs on XCD i % 8, so one XCD's CUs work on one bucket at a
+// time and its L2 holds that W32 slice). The bucket's nonempty-feature bitmap (2^sb bits) is
+// staged in LDS: an entry whose R row is empty (57% of KDD2012 entries) gets D = 0 without an L2
+// request, the others gather their W32 word. Runs are walked 16 at a time per wave (4 lanes per
+// run, up to 8 elements per lane in flight), so no element -> run map is needed.
+constexpr int kGatherGroup = 1024;  // tiles per gather workgroup
+constexpr int kGBlock = 512;        // 8 waves share one staged bitmap (64 KB at 2^19 features)
+__global__ void __launch_bounds__(kGBlock)
+lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__ BM, const int64_t* __restrict__ TE,
+                  unsigned n_tiles, int sb, int nb, uint32_t ostride, unsigned groups,
+                  const uint16_t* __restrict__ OFFT, const uint32_t* __restrict__ S, uint32_t* __restrict__ D) {
+    extern __shared__ __align__(16) uint32_t s_bm[];  // 2^sb bits
+    const unsigned xcd = blockIdx.x & 7u, k = blockIdx.x >> 3;
+    const unsigned b = xcd + 8u * (k / groups);
+    if (b >= (unsigned)nb) return;  // uniform
+    const unsigned g = k % groups;
+    const uint32_t nwords = 1u << (sb - 5);
+    const uint4* src = reinterpret_cast<const uint4*>(BM + ((size_t)b << (sb - 5)));
+    for (uint32_t i = threadIdx.x; i < nwords / 4; i += kGBlock) reinterpret_cast<uint4*>(s_bm)[i] = src[i];
+    __syncthreads();
+    const uint32_t mask = (1u << sb) - 1u;
+    const uint32_t hi = b << sb;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned t_lo = g * kGatherGroup, t_hi = std::min<unsigned>(n_tiles, t_lo + kGatherGroup);
+    constexpr int kE = 8;  // elements per lane in flight
+    for (unsigned t0 = t_lo + 16u * w; t0 < t_hi; t0 += 16u * (kGBlock / 64)) {
+        const unsigned t = t0 + (lane >> 2);
+        uint32_t st = 0, en = 0;
+        int64_t base = 0;
+        if (t < t_hi) {
+            st = OFFT[(size_t)b * ostride + t];
+            en = OFFT[(size_t)(b + 1) * ostride + t];
+            base = TE[t];
+        }
+        for (uint32_t c0 = st + (lane & 3); c0 < en; c0 += 4 * kE) {
+            uint32_t v[kE];
+#pragma unroll
+            for (int u = 0; u < kE; ++u) {
+                const uint32_t c = c0 + 4 * u;
+                v[u] = c < en ? S[base + c] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kE; ++u) {
+                const uint32_t col = v[u] & mask;
+                const bool hit = (s_bm[col >> 5] >> (col & 31)) & 1u;
+                v[u] = (c0 + 4 * u < en && hit) ? W32[hi | col] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kE; ++u) {
+                const uint32_t c = c0 + 4 * u;
+                if (c < en) D[base + c] = v[u];
+            }
+        }
+    }
+}
+
 // Deferred tiles: prefix from the (now final) look-back states, then the parked slot is copied to
 // its place. Grid-stride over the deferred list; every state is published when this runs.
 template <typename T, typename OP, typename OI>
@@ -955,7 +1029,7 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
 // Per-row semantics are scipy's csr_matmat exactly: first touch = product order, sums start at +0
 // and add in product order, sum != 0 kept.
 constexpr int kLprRows = 256;      // rows per tile (4 waves x 64 rows)
-constexpr int kLprSide = 128;      // 64-bit W words of features with > 2 R entries, per tile
+constexpr int kLprSide = 96;       // features with > 2 R entries per tile (KDD2012: 56 +- 7.5; more -> heavy)
 constexpr int kLprFlagWords = kCapAMax / 64 + 1;  // row-start bitmap words per wave
 
 struct LprSpace {
@@ -973,18 +1047,11 @@ struct LprSpace {
 __device__ __forceinline__ uint32_t lpr_h2(uint32_t col) { return (col * 0x9E3779B1u) >> 26; }
 
 // products of an entry with LDS descriptor d: bits 30-31 = n <= 2 inline 15-bit slots (sign << 14 |
-// col) in R's storage order; n = 3: the W word in side[d & mask] (<= 4 inline, or an O record)
-__device__ __forceinline__ uint32_t lpr_count(uint32_t d, const uint64_t* side, const uint16_t* O) {
-    const uint32_t n = d >> 30;
-    if (n < 3) return n;
-    const uint64_t w = side[d & 0x3fffffffu];
-    const uint32_t nw = (uint32_t)(w >> 61);
-    return nw != 7 ? nw : O[w & kLow61];
-}
+// col) in R's storage order; n = 3: the W word in side[d & mask] (<= 4 inline, or an O record).
 // t-th product's (sign << 14 | col)
 __device__ __forceinline__ uint32_t lpr_slot(uint32_t d, uint32_t t, const uint64_t* side, const uint16_t* O) {
     if ((d >> 30) < 3) return (d >> (15 * t)) & 0x7fffu;
-    const uint64_t w = side[d & 0x3fffffffu];
+    const uint64_t w = side[d & kW32J];
     if ((w >> 61) != 7) return (uint32_t)(w >> (15 * t)) & 0x7fffu;
     const uint32_t e = O[(w & kLow61) + 1 + t];
     return ((e & 0x8000u) >> 1) | (e & 0x3fffu);
@@ -1019,6 +1086,10 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     extern __shared__ __align__(16) unsigned char lds[];          // s_desc[cap_a] u32
     __shared__ uint16_t s_rowptr[kLprRows + 1];
     __shared__ uint64_t s_side[kLprSide];
+    __shared__ uint32_t s_sidej[kLprSide];                          // side entry's feature (staged)
+    __shared__ uint16_t s_sfk[kLprSide];                            // side entry's slot position
+    __shared__ uint8_t s_sfw[kLprSide];                             // ... in the slot of this wave
+    __shared__ T s_sfx[kLprSide];                                   // ... and its value
     __shared__ uint64_t s_flag[4][kLprFlagWords];                  // row-start bitmap per wave
     __shared__ uint64_t s_susp[4];                                  // rows flagged for the exact path
     __shared__ uint16_t s_kst[4][64];
@@ -1027,6 +1098,8 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     __shared__ int s_bad;
     uint32_t* s_desc = reinterpret_cast<uint32_t*>(lds);
     uint16_t* s_colbuf = reinterpret_cast<uint16_t*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)));  // 4 x slot
+    T* s_valbuf = reinterpret_cast<T*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)) +
+                                       ((8 * (size_t)sp.slot + 15) & ~size_t(15)));                // 4 x slot
 
     const unsigned tile = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1049,18 +1122,27 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     }
     STAMP(0);
     const uint32_t ne = (uint32_t)ne64;
-    for (int r = tid; r <= nrows; r += kLprRows) s_rowptr[r] = (uint16_t)((int64_t)Ap[row0 + r] - ea);
+    // row pointers in flight together with step A's loads (stored to LDS after them)
+    const int64_t rp0 = tid <= nrows ? (int64_t)Ap[row0 + tid] : 0;
+    const int64_t rp1 = tid == 0 && nrows == kLprRows ? (int64_t)Ap[row0 + kLprRows] : 0;
     // ---- step A: R descriptors of the tile's entries into LDS, by entry
-    auto put_desc = [&](uint32_t e, uint64_t w) {  // w: a W word (n <= 2 fits the 32-bit form)
-        const uint32_t n = (uint32_t)(w >> 61);
-        uint32_t d = (n << 30) | (uint32_t)(w & 0x3fffffffu);
-        if (n > 2) {
-            const uint32_t k = atomicAdd(&s_nside, 1u);
-            if (k < (uint32_t)kLprSide) s_side[k] = w;
-            else s_bad = 1;
-            d = 0xc0000000u | k;
+    // LDS descriptor of an entry: n <= 2 -> the W32 form (count, two inline 15-bit slots);
+    // more entries -> code 3 | count (4 bits) << 26 | side index: the feature's W word lands in
+    // s_side[k] (direct: now; staged: gathered after step A, needed only after the flat pass)
+    auto put_side = [&](uint32_t e, uint32_t c4, uint32_t j_or_0, uint64_t w, bool have_w) {
+        const uint32_t k = atomicAdd(&s_nside, 1u);
+        if (k < (uint32_t)kLprSide) {
+            if (have_w) s_side[k] = w;
+            s_sidej[k] = j_or_0;
+        } else {
+            s_bad = 1;
         }
-        s_desc[e] = d;
+        s_desc[e] = 0xc0000000u | (c4 << 26) | k;
+    };
+    auto put_desc = [&](uint32_t e, uint64_t w) {  // direct mode: the W word itself
+        const uint32_t n = (uint32_t)(w >> 61);
+        if (n <= 2) s_desc[e] = (n << 30) | (uint32_t)(w & 0x3fffffffu);
+        else put_side(e, std::min(n != 7 ? n : (uint32_t)R.O[w & kLow61], 15u), 0u, w, true);
     };
     constexpr int kU = 12;  // loads of a round issued before any is used
     if constexpr (STAGED) {
@@ -1075,14 +1157,10 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
                 sv[u] = q < ne ? St[q] : 0u;
                 dv[u] = q < ne ? Dt[q] : 0u;
             }
-            uint64_t wv[kU];  // code 3: the full W word of a feature with > 2 entries
-#pragma unroll
-            for (int u = 0; u < kU; ++u)
-                wv[u] = (q0 + u * kLprRows < ne && (dv[u] >> 30) == 3) ? R.W[dv[u] & 0x3fffffffu] : 0ull;
 #pragma unroll
             for (int u = 0; u < kU; ++u)
                 if (q0 + u * kLprRows < ne) {
-                    if ((dv[u] >> 30) == 3) put_desc(sv[u] >> 20, wv[u]);
+                    if ((dv[u] >> 30) == 3) put_side(sv[u] >> 20, (dv[u] >> 26) & 15u, dv[u] & kW32J, 0ull, false);
                     else s_desc[sv[u] >> 20] = dv[u];  // the W32 word: same bits as W's slots 0-1
                 }
         }
@@ -1103,6 +1181,8 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
                 if (q0 + u * kLprRows < ne) put_desc(q0 + u * kLprRows, w[u]);
         }
     }
+    if (tid <= nrows) s_rowptr[tid] = (uint16_t)(rp0 - ea);
+    if (tid == 0 && nrows == kLprRows) s_rowptr[kLprRows] = (uint16_t)(rp1 - ea);
     STAMP(1);
     __syncthreads();
     STAMP(2);
@@ -1110,6 +1190,11 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         if (tid == 0) go_heavy();
         return;
     }
+    // staged: the W words of the side entries are gathered now and only needed after the flat
+    // pass (their counts came with the staged words), so this latency hides behind the pass
+    const uint32_t nside = s_nside;
+    uint64_t sidew = 0;
+    if (STAGED && (uint32_t)tid < nside) sidew = R.W[s_sidej[tid]];
     // ---- step B: one wave per 64 rows, one flat pass over the wave's entries
     const int w = tid >> 6, lane = tid & 63;
     const int r = tid;  // this lane's row (for per-row work)
@@ -1129,9 +1214,11 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         s_nz2row[w][__builtin_popcountll(ne_mask & ((1ull << lane) - 1))] = (uint8_t)lane;
     }
     __builtin_amdgcn_wave_barrier();
-    uint16_t* __restrict__ oc = sp.cols + ((size_t)tile * 4 + w) * sp.slot;
-    T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + ((size_t)tile * 4 + w) * sp.slot;
-    uint16_t* cb = s_colbuf + (size_t)w * sp.slot;  // the wave's kept columns, slot order
+    // the wave's slot is built in LDS (columns cb, values vb, first-touch order) and stored to
+    // HBM with coalesced stores at the end: no global store inside the pass, so the compiler's
+    // vmcnt accounting keeps the value prefetch in flight
+    uint16_t* cb = s_colbuf + (size_t)w * sp.slot;
+    T* vb = s_valbuf + (size_t)w * sp.slot;
     const T* __restrict__ Axw = Ax + ea;
     uint32_t carry_r = 0, carry_k = 0;
     const T nmag = -mag;
@@ -1143,7 +1230,7 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         const uint32_t row = s_nz2row[w][nr & 63];
         const uint32_t d = ve ? s_desc[e] : 0u;
         const uint32_t n = d >> 30;
-        const uint32_t np = n < 3 ? n : lpr_count(d, s_side, R.O);  // n == 3: a side entry (rare)
+        const uint32_t np = n < 3 ? n : (d >> 26) & 15u;  // n == 3: a side entry (count in the word)
         const bool nzx = tmul<T>(x, mag) != T(0);  // all products of an entry share |x * mag|
         const uint32_t kc = nzx ? np : 0u;
         const uint32_t kinc = wave_scan_dpp(kc);
@@ -1151,32 +1238,34 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         if (ve && ((fw >> lane) & 1ull)) s_kst[w][row] = (uint16_t)K;  // the row's first entry
         const uint32_t sl0 = d & 0x7fffu, sl1 = (d >> 15) & 0x7fffu;
         if (n < 3 && kc >= 1 && K < sp.slot) {
-            oc[K] = (uint16_t)(sl0 & 0x3fffu);
-            ov[K] = tadd<T>(T(0), tmul<T>(x, (sl0 & 0x4000u) ? nmag : mag));
             cb[K] = (uint16_t)(sl0 & 0x3fffu);
+            vb[K] = tadd<T>(T(0), tmul<T>(x, (sl0 & 0x4000u) ? nmag : mag));
         }
         if (n < 3 && kc >= 2 && K + 1 < sp.slot) {
-            oc[K + 1] = (uint16_t)(sl1 & 0x3fffu);
-            ov[K + 1] = tadd<T>(T(0), tmul<T>(x, (sl1 & 0x4000u) ? nmag : mag));
             cb[K + 1] = (uint16_t)(sl1 & 0x3fffu);
+            vb[K + 1] = tadd<T>(T(0), tmul<T>(x, (sl1 & 0x4000u) ? nmag : mag));
         }
-        if (__ballot(n == 3 && kc > 0)) {  // side entries: every product in R's storage order
-            if (n == 3 && kc > 0)
-                for (uint32_t t = 0; t < np && K + t < sp.slot; ++t) {
-                    const uint32_t sl = lpr_slot(d, t, s_side, R.O);
-                    oc[K + t] = (uint16_t)(sl & 0x3fffu);
-                    ov[K + t] = tadd<T>(T(0), tmul<T>(x, (sl & 0x4000u) ? nmag : mag));
-                    cb[K + t] = (uint16_t)(sl & 0x3fffu);
-                }
+        // side entries keep a gap [K, K + np) in the slot, filled after the pass (their W words
+        // may still be in flight); a zero product is not in the slot: its row takes the exact path
+        if (n == 3) {
+            const uint32_t k = d & kW32J;
+            s_sfk[k] = kc ? (uint16_t)K : (uint16_t)0xffffu;
+            s_sfw[k] = (uint8_t)w;
+            s_sfx[k] = x;
+            if (np == 15) s_bad = 1;  // 15 or more entries: the count is not exact -> heavy tile
         }
-        // a zero product (x == 0, or underflow) is not in the slot: its row takes the exact path,
-        // which sees every product
         if (ve && np > 0 && !nzx) atomicOr(reinterpret_cast<unsigned long long*>(&s_susp[w]), 1ull << row);
         carry_k += __builtin_amdgcn_readlane(kinc, 63);
         carry_r += (uint32_t)__builtin_popcountll(fw);
     };
     // values straight from HBM in entry order (coalesced), four steps in flight ahead of use
-    auto ldx = [&](uint32_t j) { const uint32_t e = E0 + 64 * j + lane; return e < E1 ? Axw[e] : T(0); };
+    // unconditional loads (index clamped, value masked): straight-line vmcnt accounting
+    const uint32_t elast = E1 > E0 ? E1 - 1 : E0;
+    auto ldx = [&](uint32_t j) {
+        const uint32_t e = E0 + 64 * j + lane;
+        const T v = Axw[std::min(e, elast)];
+        return e < E1 ? v : T(0);
+    };
     T x0 = ldx(0), x1 = ldx(1), x2 = ldx(2), x3 = ldx(3);
     for (uint32_t j = 0; j < nsteps; j += 4) {
         T c0 = x0, c1 = x1, c2 = x2, c3 = x3;
@@ -1190,7 +1279,36 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         if (j + 3 < nsteps) step(j + 3, c3);
     }
     bool overflow = carry_k > sp.slot;
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
+    // side fill: every side entry's products into its gap, in R's storage order
+    if ((uint32_t)tid < nside) {
+        const uint64_t sw = STAGED ? sidew : s_side[tid];
+        if (STAGED) s_side[tid] = sw;
+        const uint32_t k0 = s_sfk[tid];
+        if (k0 != 0xffffu) {
+            uint16_t* cbw = s_colbuf + (size_t)s_sfw[tid] * sp.slot;
+            T* vbw = s_valbuf + (size_t)s_sfw[tid] * sp.slot;
+            const T x = s_sfx[tid];
+            const bool rec = (sw >> 61) == 7;
+            const uint32_t np = rec ? R.O[sw & kLow61] : (uint32_t)(sw >> 61);
+            for (uint32_t t = 0; t < np && k0 + t < sp.slot; ++t) {
+                uint32_t sl;
+                if (rec) {
+                    const uint32_t e = R.O[(sw & kLow61) + 1 + t];
+                    sl = ((e & 0x8000u) >> 1) | (e & 0x3fffu);
+                } else {
+                    sl = (uint32_t)(sw >> (15 * t)) & 0x7fffu;
+                }
+                cbw[k0 + t] = (uint16_t)(sl & 0x3fffu);
+                vbw[k0 + t] = tadd<T>(T(0), tmul<T>(x, (sl & 0x4000u) ? -mag : mag));
+            }
+        }
+    }
+    __syncthreads();
+    if (s_bad) {  // uniform: a side entry with 15 or more products
+        if (tid == 0) go_heavy();
+        return;
+    }
     STAMP(3);
     // ---- per row: kept count and a Bloom check of its columns (3 x 64-bit filters in registers):
     // a column whose 3 bits are all set already flags the row for the exact path (every real
@@ -1214,10 +1332,10 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         }
     }
     uint64_t todo = s_susp[w] | __ballot(hit);  // lane == row within the wave
-    __builtin_amdgcn_wave_barrier();  // the column buffer is dead from here: the scratch reuses it
-    const int kScr = (int)((sp.slot * 2 - 16) / (2 + sizeof(T)));
-    uint16_t* scol = cb;
-    T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(cb) + ((2 * (size_t)kScr + 15) & ~size_t(15)));
+    __builtin_amdgcn_wave_barrier();  // the row-start bitmap is dead from here: the scratch reuses it
+    constexpr int kScr = (int)((kLprFlagWords * 8 - 16) / (2 + sizeof(T)));
+    uint16_t* scol = reinterpret_cast<uint16_t*>(&s_flag[w][0]);
+    T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(&s_flag[w][0]) + ((2 * kScr + 15) & ~15));
     if (__ballot(overflow)) todo = 0;
     // exact path, one flagged row at a time, the whole wave on it: its products in sequence order
     // into the scratch, then every product checks for an earlier one of its column (first touch);
@@ -1232,7 +1350,7 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             const bool in = e < a1;
             const uint32_t d = in ? s_desc[e] : 0u;
             const T x = in ? Axw[e] : T(0);
-            const uint32_t np = in ? lpr_count(d, s_side, R.O) : 0u;
+            const uint32_t np = in ? ((d >> 30) < 3 ? (d >> 30) : (d >> 26) & 15u) : 0u;
             const uint32_t inc = wave_scan_dpp(np);
             const uint32_t q0 = nprod + inc - np;
             for (uint32_t t = 0; t < np; ++t)
@@ -1267,8 +1385,8 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             if (keep) {
                 if (kR + nk + ki - 1 >= sp.slot) overflow = true;
                 else {
-                    oc[kR + nk + ki - 1] = scol[q];
-                    ov[kR + nk + ki - 1] = sum;
+                    cb[kR + nk + ki - 1] = scol[q];
+                    vb[kR + nk + ki - 1] = sum;
                 }
             }
             nk += __builtin_amdgcn_readlane(ki, 63);
@@ -1285,21 +1403,30 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     }
     if (order == RP_ORDER_SORTED && kept > 1) {  // ascending columns inside the row's slot range
         for (uint32_t a = kst + 1; a < kst + kept; ++a) {
-            const uint16_t kc = oc[a];
-            const T kv = ov[a];
+            const uint16_t kc = cb[a];
+            const T kv = vb[a];
             uint32_t b = a;
-            while (b > kst && oc[b - 1] > kc) {
-                oc[b] = oc[b - 1];
-                ov[b] = ov[b - 1];
+            while (b > kst && cb[b - 1] > kc) {
+                cb[b] = cb[b - 1];
+                vb[b] = vb[b - 1];
                 --b;
             }
-            oc[b] = kc;
-            ov[b] = kv;
+            cb[b] = kc;
+            vb[b] = kv;
         }
     }
     if (valid) sp.rowmeta[(size_t)tile * kLprRows + r] = (kst << 16) | kept;
     const uint32_t wtot = __builtin_amdgcn_readlane(wave_scan_dpp(valid ? kept : 0u), 63);
     if (lane == 0) sp.cnt[(size_t)tile * 4 + w] = wtot;
+    // the slot to HBM, coalesced (rows may end before their kept range when the exact path
+    // dropped entries: the whole used range goes, the copy kernel reads each row's own part)
+    __builtin_amdgcn_wave_barrier();
+    uint16_t* __restrict__ oc = sp.cols + ((size_t)tile * 4 + w) * sp.slot;
+    T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + ((size_t)tile * 4 + w) * sp.slot;
+    for (uint32_t q = lane; q < carry_k; q += 64) {
+        oc[q] = cb[q];
+        ov[q] = vb[q];
+    }
     STAMP(4);
     STAMP(5);
     STAMP(6);
@@ -1593,6 +1720,7 @@ struct rp_projector {
     // packed
     DevBuf W, O, spare;  // packed image: W (u64 per feature), O (long-row records); spare unused
     DevBuf W32;          // staged-gather table derived from W (u32 per feature), m < 2^30 only
+    DevBuf BM;           // nonempty-feature bitmap (1 bit per feature) for the filtered gather
     int stage_mode = -1; // -1 auto, 0 off, 1 on (rp_projector_set_staging)
     int stage_sb = 0;    // bucket = 2^sb features; 0 = auto
     // generic
@@ -1697,7 +1825,9 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
         pl.caps.cap_a = (int)std::min<double>(kCapAMax, ((int)(ents + 6.0 * std::sqrt(ents) + 40.0) + 63) & ~63);
         pl.caps.cap_p = (int)std::min<double>(65535.0, ((int)(prods + 9.5 * std::sqrt(prods) + 64.0) + 63) & ~63);
         const double prods_w = std::max(1.0, avg * 64 * ppe);  // one wave's slot: 64 rows
-        pl.lpr_slot = (uint32_t)std::min<double>(65535.0, ((int)(prods_w + 12.0 * std::sqrt(prods_w) + 64.0) + 63) & ~63);
+        // mean + 7 sigma (sigma ~ 1.25 sqrt(mean) for single-magnitude SRP rows) + 32: KDD2012 608,
+        // which keeps a tile's LDS (descriptors + the 4 slots) at 32 KB: 5 tiles per CU
+        pl.lpr_slot = (uint32_t)std::min<double>(65535.0, ((int)(prods_w + 8.75 * std::sqrt(prods_w) + 32.0) + 31) & ~31);
         pl.n_tiles = (n_rows + kLprRows - 1) / kLprRows;
         const size_t nw = 4 * (size_t)pl.n_tiles;
         pl.scan_blocks = ((int64_t)nw + kBlock * kScanPer - 1) / (kBlock * kScanPer);
@@ -1826,8 +1956,8 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
     return RP_OK;
 }
 
-size_t lpr_lds_bytes(int cap_a, size_t, uint32_t slot) {
-    return ((4 * (size_t)cap_a + 15) & ~size_t(15)) + 4 * 2 * (size_t)slot;
+size_t lpr_lds_bytes(int cap_a, size_t vs, uint32_t slot) {
+    return ((4 * (size_t)cap_a + 15) & ~size_t(15)) + ((8 * (size_t)slot + 15) & ~size_t(15)) + 4 * vs * (size_t)slot;
 }
 
 template <typename T, typename IP, typename OP, typename OI>
@@ -1855,11 +1985,13 @@ int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, con
                            st, Ap, a->indices, Ax, a->n_rows, pl.caps, n_tiles, pl.sb, pl.nb, pl.ostride, Sw,
                            (T*)nullptr, OFFT, TE);
         HIP_TRY(hipGetLastError());
-        const unsigned groups = (n_tiles + kStageTB - 1) / kStageTB;
+        const unsigned groups = (n_tiles + kGatherGroup - 1) / kGatherGroup;
         const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * groups;
-        hipLaunchKernelGGL(stage_gather_kernel, dim3(grid), dim3(kBlock), kStageMap, st, (const uint32_t*)h->W32.p,
-                           (const int64_t*)TE, n_tiles, pl.sb, pl.nb, pl.ostride, groups, (const uint16_t*)OFFT,
-                           (const uint32_t*)Sw, Dw);
+        const size_t glds = (size_t)4 << (pl.sb - 5);
+        HIP_TRY(hipFuncSetAttribute((const void*)lpr_gather_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds));
+        hipLaunchKernelGGL(lpr_gather_kernel, dim3(grid), dim3(kGBlock), glds, st, (const uint32_t*)h->W32.p,
+                           (const uint32_t*)h->BM.p, (const int64_t*)TE, n_tiles, pl.sb, pl.nb, pl.ostride, groups,
+                           (const uint16_t*)OFFT, (const uint32_t*)Sw, Dw);
         HIP_TRY(hipGetLastError());
         S = Sw;
         D = Dw;
@@ -2185,11 +2317,19 @@ int rp_device_count(int* count) {
 namespace {
 // the staged-gather table (u32 per feature) derived from the uploaded W
 int build_w32(rp_projector* h) {
-    if (h->layout != RP_LAYOUT_PACKED || h->m <= 0 || h->m >= ((int64_t)1 << 30)) return RP_OK;
+    if (h->layout != RP_LAYOUT_PACKED || h->m <= 0 || h->m > ((int64_t)1 << 26)) return RP_OK;
     int rc = h->W32.ensure(4 * (size_t)h->m, h->device);
     if (rc) return rc;
     hipLaunchKernelGGL(build_w32_kernel, dim3(2048), dim3(256), 0, nullptr, (const uint64_t*)h->W.p,
-                       (uint32_t*)h->W32.p, h->m);
+                       (const uint16_t*)h->O.p, (uint32_t*)h->W32.p, h->m);
+    HIP_TRY(hipGetLastError());
+    // bitmap padded to whole 2^20-feature slices so a gather workgroup can stage any slice
+    const size_t bm_words = (size_t)((h->m + (1 << 20) - 1) >> 20) << 15;
+    rc = h->BM.ensure(4 * bm_words, h->device);
+    if (rc) return rc;
+    HIP_TRY(hipMemset(h->BM.p, 0, 4 * bm_words));
+    hipLaunchKernelGGL(build_bitmap_kernel, dim3(2048), dim3(256), 0, nullptr, (const uint64_t*)h->W.p,
+                       (uint32_t*)h->BM.p, h->m);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipDeviceSynchronize());
     return RP_OK;
@@ -2384,7 +2524,7 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
     if (bucket_shift != 0 && (bucket_shift < 1 || bucket_shift > 20))
         return fail(RP_ERR_INVALID, "bucket_shift must be 0 (auto) or in [1, 20]");
     if (mode == 1 && !h->W32.p)
-        return fail(RP_ERR_UNSUPPORTED, "staged gather needs the packed layout and m < 2^30");
+        return fail(RP_ERR_UNSUPPORTED, "staged gather needs the packed layout and m <= 2^26");
     const int sb = bucket_shift > 0 ? bucket_shift : 20;
     if (mode == 1 && ((h->m + ((int64_t)1 << sb) - 1) >> sb) > kStageMaxNB)
         return fail(RP_ERR_INVALID, "m=%lld needs more than %d buckets of 2^%d features", (long long)h->m,
