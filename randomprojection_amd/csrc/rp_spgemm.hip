@@ -912,59 +912,208 @@ stage_gather_kernel(const uint32_t* __restrict__ W32, const int64_t* __restrict_
     }
 }
 
-// Filtered staged gather for the row-lane pipeline. Workgroup (bucket b, tile group g) on XCD b % 8
-// (round-robin dispatch: workgroup i runs on XCD i % 8, so one XCD's CUs work on one bucket at a
-// time and its L2 holds that W32 slice). The bucket's nonempty-feature bitmap (2^sb bits) is
-// staged in LDS: an entry whose R row is empty (57% of KDD2012 entries) gets D = 0 without an L2
-// request, the others gather their W32 word. Runs are walked 16 at a time per wave (4 lanes per
-// run, up to 8 elements per lane in flight), so no element -> run map is needed.
-constexpr int kGatherGroup = 1024;  // tiles per gather workgroup
-constexpr int kGBlock = 512;        // 8 waves share one staged bitmap (64 KB at 2^19 features)
+// ---- staging for the row-lane pipeline: bucket-major runs inside groups of kRunGroup tiles.
+// S holds, for tile group g and bucket b, the entries of all the group's tiles whose feature falls
+// in b as ONE contiguous segment (tile order, then rank order inside the tile); segments are laid
+// out in (g, b) order. So the gather streams whole segments (full 128-byte lines, nothing shared
+// between workgroups), and a tile's entries come back as nb runs, each adjacent to the neighbouring
+// tiles' runs of the same bucket — neighbours run on the same XCD (xcd_tile), so the lines they
+// share meet in one L2. Index arrays (workspace):
+//   OFFT[b][t] (u16)  within-tile start of bucket b (bucket order), OFFT[nb][t] = the tile's entries
+//   OFF2[b][t] (u32)  start of tile t's run in segment (g, b), relative to the segment
+//   GB[g*nb + b] (i64) segment start in S (exclusive prefix; GB[groups*nb] = all staged entries)
+// A tile past the entry cap stages nothing (its counts are 0): the heavy path reads A itself.
+constexpr int kRunGroup = 4096;  // tiles per group (uniform KDD2012: ~110K entries per segment)
+
+// XCD-aware tile order: workgroup i runs on XCD i % 8 (round-robin dispatch); XCD x takes tiles
+// [x * t8, (x + 1) * t8) in order, so neighbouring tiles are in flight on one XCD together
+__device__ __forceinline__ unsigned xcd_tile(unsigned i, unsigned t8) { return (i & 7u) * t8 + (i >> 3); }
+
+// K1: per-tile bucket histogram -> OFFT (within-tile exclusive starts)
+template <typename IP>
+__global__ void __launch_bounds__(kBlock)
+lpr_count_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, Caps caps,
+                 unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT) {
+    __shared__ uint32_t s_hist[kStageMaxNB];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    const int tid = threadIdx.x;
+    const unsigned t = xcd_tile(blockIdx.x, t8);
+    if (t >= n_tiles) return;  // uniform
+    const int64_t row0 = (int64_t)t * caps.rpt;
+    const int64_t ea = (int64_t)Ap[row0];
+    const int64_t ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
+    if (ne > caps.cap_a) {
+        for (int b = tid; b <= nb; b += kBlock) OFFT[(size_t)b * ostride + t] = 0;
+        return;
+    }
+    const uint32_t n = (uint32_t)ne;
+    if (tid < nb) s_hist[tid] = 0;
+    __syncthreads();
+    const int32_t* __restrict__ Ajt = Aj + ea;
+    int32_t jj[kMaxE];
+#pragma unroll
+    for (int i = 0; i < kMaxE; ++i) {
+        const uint32_t e = tid + i * kBlock;
+        jj[i] = e < n ? Ajt[e] : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < kMaxE; ++i)
+        if (jj[i] >= 0) atomicAdd(&s_hist[(uint32_t)jj[i] >> sb], 1u);
+    __syncthreads();
+    uint32_t tot;
+    const uint32_t base = block_excl_scan(tid < nb ? s_hist[tid] : 0u, s_wsum, &tot);
+    if (tid < nb) OFFT[(size_t)tid * ostride + t] = (uint16_t)base;
+    if (tid == 0) OFFT[(size_t)nb * ostride + t] = (uint16_t)n;
+}
+
+// K2: one workgroup per (group, bucket): runs of the group's tiles -> OFF2, segment size -> GB
+constexpr int kRunPer = kRunGroup / kBlock;  // tiles per thread
+__global__ void __launch_bounds__(kBlock)
+lpr_run_scan_kernel(const uint16_t* __restrict__ OFFT, uint32_t* __restrict__ OFF2, int64_t* __restrict__ GB,
+                    unsigned n_tiles, int nb, uint32_t ostride) {
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    const unsigned g = blockIdx.x / (unsigned)nb, b = blockIdx.x % (unsigned)nb;
+    const unsigned t0 = g * kRunGroup + kRunPer * threadIdx.x;
+    const uint16_t* o0 = OFFT + (size_t)b * ostride;
+    const uint16_t* o1 = o0 + ostride;
+    uint32_t c[kRunPer], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kRunPer; ++i) {
+        const unsigned t = t0 + i;
+        c[i] = t < n_tiles ? (uint32_t)o1[t] - (uint32_t)o0[t] : 0u;
+        sum += c[i];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan(sum, s_wsum, &tot);
+#pragma unroll
+    for (int i = 0; i < kRunPer; ++i) {
+        const unsigned t = t0 + i;
+        if (t < n_tiles) OFF2[(size_t)b * ostride + t] = run;
+        run += c[i];
+    }
+    if (threadIdx.x == 0) GB[blockIdx.x] = tot;
+}
+
+// K3: segment sizes -> exclusive starts, in place (one workgroup of 1024 threads)
+__global__ void __launch_bounds__(1024) lpr_seg_scan_kernel(int64_t* __restrict__ GB, unsigned n) {
+    __shared__ int64_t s[1024];
+    const unsigned per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = std::min(n, lo + per);
+    int64_t sum = 0;
+    for (unsigned i = lo; i < hi; ++i) sum += GB[i];
+    s[threadIdx.x] = sum;
+    __syncthreads();
+    for (unsigned o = 1; o < 1024; o <<= 1) {
+        const int64_t v = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+        __syncthreads();
+        s[threadIdx.x] += v;
+        __syncthreads();
+    }
+    int64_t run = s[threadIdx.x] - sum;
+    for (unsigned i = lo; i < hi; ++i) {
+        const int64_t v = GB[i];
+        GB[i] = run;
+        run += v;
+    }
+    if (threadIdx.x == 1023) GB[n] = s[1023];
+}
+
+// largest b in [0, nb] with st[b] <= q (fixed trip count: 9 probes cover nb <= 256)
+__device__ __forceinline__ uint32_t run_of(const uint16_t* st, int nb, uint32_t q) {
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 256; step; step >>= 1)
+        if (lo + step <= (uint32_t)nb && st[lo + step] <= q) lo += step;
+    return lo;
+}
+
+// K4: the tile's entries ranked into bucket order in LDS, then written to their runs (consecutive
+// lanes -> consecutive S words inside a run). S word: entry index in the tile << 20 | column bits.
+template <typename IP>
+__global__ void __launch_bounds__(kBlock)
+lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, Caps caps,
+                     unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride,
+                     const uint16_t* __restrict__ OFFT, const uint32_t* __restrict__ OFF2,
+                     const int64_t* __restrict__ GB, uint32_t* __restrict__ S) {
+    extern __shared__ __align__(16) uint32_t s_key[];  // [cap_a]
+    __shared__ uint32_t s_cur[kStageMaxNB];
+    __shared__ uint16_t s_st[kStageMaxNB + 1];
+    __shared__ int64_t s_dst[kStageMaxNB];
+    const int tid = threadIdx.x;
+    const unsigned t = xcd_tile(blockIdx.x, t8);
+    if (t >= n_tiles) return;  // uniform
+    const int64_t row0 = (int64_t)t * caps.rpt;
+    const int64_t ea = (int64_t)Ap[row0];
+    const int64_t ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
+    if (ne > caps.cap_a) return;  // uniform: heavy tile, no runs
+    const uint32_t n = (uint32_t)ne;
+    const int32_t* __restrict__ Ajt = Aj + ea;
+    int32_t jj[kMaxE];
+#pragma unroll
+    for (int i = 0; i < kMaxE; ++i) {
+        const uint32_t e = tid + i * kBlock;
+        jj[i] = e < n ? Ajt[e] : -1;
+    }
+    const size_t gb = (size_t)(t / kRunGroup) * nb;
+    if (tid < nb) {
+        const uint32_t st = OFFT[(size_t)tid * ostride + t];
+        s_st[tid] = (uint16_t)st;
+        s_cur[tid] = st;
+        s_dst[tid] = GB[gb + tid] + (int64_t)OFF2[(size_t)tid * ostride + t] - (int64_t)st;
+    }
+    if (tid == 0) s_st[nb] = (uint16_t)n;
+    __syncthreads();
+    const uint32_t mask = (1u << sb) - 1u;
+#pragma unroll
+    for (int i = 0; i < kMaxE; ++i)
+        if (jj[i] >= 0) {
+            const uint32_t pos = atomicAdd(&s_cur[(uint32_t)jj[i] >> sb], 1u);
+            s_key[pos] = ((tid + i * kBlock) << 20) | ((uint32_t)jj[i] & mask);
+        }
+    __syncthreads();
+    for (uint32_t q = tid; q < n; q += kBlock) S[s_dst[run_of(s_st, nb, q)] + q] = s_key[q];
+}
+
+// K5: filtered gather, one workgroup per (bucket b, group g) segment, on XCD b % 8 (workgroup i
+// runs on XCD i % 8, so one XCD's CUs work on one bucket at a time and its L2 holds that W32
+// slice). The bucket's nonempty-feature bitmap (2^sb bits) is staged in LDS: an entry whose R row
+// is empty (57% of KDD2012 entries) gets D = 0 without an L2 request, the others gather their
+// W32 word. S in, D out: both streamed whole-line.
+constexpr int kGBlock = 512;  // 8 waves share one staged bitmap (64 KB at 2^19 features)
 __global__ void __launch_bounds__(kGBlock)
-lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__ BM, const int64_t* __restrict__ TE,
-                  unsigned n_tiles, int sb, int nb, uint32_t ostride, unsigned groups,
-                  const uint16_t* __restrict__ OFFT, const uint32_t* __restrict__ S, uint32_t* __restrict__ D) {
+lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__ BM, const int64_t* __restrict__ GB,
+                  int sb, int nb, unsigned groups, const uint32_t* __restrict__ S, uint32_t* __restrict__ D) {
     extern __shared__ __align__(16) uint32_t s_bm[];  // 2^sb bits
     const unsigned xcd = blockIdx.x & 7u, k = blockIdx.x >> 3;
     const unsigned b = xcd + 8u * (k / groups);
     if (b >= (unsigned)nb) return;  // uniform
     const unsigned g = k % groups;
+    const int64_t lo = GB[(size_t)g * nb + b], hi = GB[(size_t)g * nb + b + 1];
+    if (lo == hi) return;
     const uint32_t nwords = 1u << (sb - 5);
     const uint4* src = reinterpret_cast<const uint4*>(BM + ((size_t)b << (sb - 5)));
     for (uint32_t i = threadIdx.x; i < nwords / 4; i += kGBlock) reinterpret_cast<uint4*>(s_bm)[i] = src[i];
     __syncthreads();
     const uint32_t mask = (1u << sb) - 1u;
-    const uint32_t hi = b << sb;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const unsigned t_lo = g * kGatherGroup, t_hi = std::min<unsigned>(n_tiles, t_lo + kGatherGroup);
-    constexpr int kE = 8;  // elements per lane in flight
-    for (unsigned t0 = t_lo + 16u * w; t0 < t_hi; t0 += 16u * (kGBlock / 64)) {
-        const unsigned t = t0 + (lane >> 2);
-        uint32_t st = 0, en = 0;
-        int64_t base = 0;
-        if (t < t_hi) {
-            st = OFFT[(size_t)b * ostride + t];
-            en = OFFT[(size_t)(b + 1) * ostride + t];
-            base = TE[t];
+    const uint32_t wb = b << sb;
+    constexpr int kU = 8;
+    for (int64_t f0 = (lo & ~int64_t(31)) + threadIdx.x; f0 < hi; f0 += kU * kGBlock) {
+        uint32_t v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int64_t f = f0 + u * kGBlock;
+            v[u] = f >= lo && f < hi ? S[f] : 0u;
         }
-        for (uint32_t c0 = st + (lane & 3); c0 < en; c0 += 4 * kE) {
-            uint32_t v[kE];
 #pragma unroll
-            for (int u = 0; u < kE; ++u) {
-                const uint32_t c = c0 + 4 * u;
-                v[u] = c < en ? S[base + c] : 0u;
-            }
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t col = v[u] & mask;
+            const int64_t f = f0 + u * kGBlock;
+            const bool hit = (s_bm[col >> 5] >> (col & 31)) & 1u;
+            v[u] = (f >= lo && f < hi && hit) ? W32[wb | col] : 0u;
+        }
 #pragma unroll
-            for (int u = 0; u < kE; ++u) {
-                const uint32_t col = v[u] & mask;
-                const bool hit = (s_bm[col >> 5] >> (col & 31)) & 1u;
-                v[u] = (c0 + 4 * u < en && hit) ? W32[hi | col] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < kE; ++u) {
-                const uint32_t c = c0 + 4 * u;
-                if (c < en) D[base + c] = v[u];
-            }
+        for (int u = 0; u < kU; ++u) {
+            const int64_t f = f0 + u * kGBlock;
+            if (f >= lo && f < hi) D[f] = v[u];
         }
     }
 }
@@ -1078,11 +1227,22 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
     return v;
 }
 
+// staged runs of the row-lane pipeline (see lpr_partition_kernel)
+struct LprStage {
+    const uint16_t* offt;
+    const uint32_t* off2;
+    const int64_t* gb;
+    const uint32_t* s;
+    const uint32_t* d;
+    uint32_t ostride;
+    int nb;
+};
+
 template <typename T, typename IP, bool STAGED>
 __global__ void __launch_bounds__(kLprRows)
 lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
-                const T* __restrict__ Ax, const uint32_t* __restrict__ S, const uint32_t* __restrict__ D,
-                int cap_a, unsigned n_tiles, int order, LprSpace sp, Workspace* ws) {
+                const T* __restrict__ Ax, LprStage stg, int cap_a, unsigned n_tiles, unsigned t8, int order,
+                LprSpace sp, Workspace* ws) {
     extern __shared__ __align__(16) unsigned char lds[];          // s_desc[cap_a] u32
     __shared__ uint16_t s_rowptr[kLprRows + 1];
     __shared__ uint64_t s_side[kLprSide];
@@ -1094,14 +1254,15 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     __shared__ uint64_t s_susp[4];                                  // rows flagged for the exact path
     __shared__ uint16_t s_kst[4][64];
     __shared__ uint8_t s_nz2row[4][64];
-    __shared__ uint32_t s_nside, s_scr[4];
+    __shared__ uint32_t s_nside, s_scr[4], s_wnz[4];
     __shared__ int s_bad;
     uint32_t* s_desc = reinterpret_cast<uint32_t*>(lds);
     uint16_t* s_colbuf = reinterpret_cast<uint16_t*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)));  // 4 x slot
     T* s_valbuf = reinterpret_cast<T*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)) +
                                        ((8 * (size_t)sp.slot + 15) & ~size_t(15)));                // 4 x slot
 
-    const unsigned tile = blockIdx.x;
+    const unsigned tile = xcd_tile(blockIdx.x, t8);
+    if (tile >= n_tiles) return;  // uniform
     const int tid = threadIdx.x;
     const int64_t row0 = (int64_t)tile * kLprRows;
     const int nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
@@ -1112,6 +1273,29 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         s_bad = ne64 > cap_a;
     }
     if (tid < 4) s_scr[tid] = 0;
+    // staged: the tile's run table, loaded together with the row pointers. Run b holds the entries
+    // q in [st_b, st_b + len_b) (bucket order) at S/D index src_b + q - st_b, relative to the
+    // group's first segment. Element -> run: bit q of s_sbm marks the start of a nonempty run, so
+    // the k-th nonempty run holds q for k = (set bits at or below q) - 1, and s_ksrc[k] gives its
+    // index offset. Both live in the slot buffers, which the flat pass fills only later.
+    uint32_t* s_ksrc = reinterpret_cast<uint32_t*>(s_colbuf);
+    uint64_t* s_sbm = reinterpret_cast<uint64_t*>(s_colbuf + 2 * kStageMaxNB);
+    uint32_t m_st = 0, m_len = 0, m_src = 0;
+    uint64_t nzb = 0;
+    int64_t g0 = 0;
+    if constexpr (STAGED) {
+        const size_t gb = (size_t)(tile / kRunGroup) * stg.nb;
+        g0 = stg.gb[gb];
+        if (tid < stg.nb) {
+            const size_t o = (size_t)tid * stg.ostride + tile;
+            m_st = stg.offt[o];
+            m_len = stg.offt[o + stg.ostride] - m_st;
+            m_src = (uint32_t)(stg.gb[gb + tid] - g0) + stg.off2[o];
+        }
+        if (tid < 64) s_sbm[tid] = 0ull;
+        nzb = __ballot(m_len > 0);
+        if ((tid & 63) == 0) s_wnz[tid >> 6] = (uint32_t)__popcll(nzb);
+    }
     __syncthreads();
     auto go_heavy = [&]() {  // one lane of the tile: the heavy path takes the whole tile
         if (atomicOr(&sp.tflag[tile], 1u) == 0u) sp.hlist[atomicAdd(&ws->n_deferred, 1u)] = tile;
@@ -1146,16 +1330,28 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     };
     constexpr int kU = 12;  // loads of a round issued before any is used
     if constexpr (STAGED) {
-        const int64_t qb = ea - (int64_t)Ap[0];
-        const uint32_t* __restrict__ St = S + qb;
-        const uint32_t* __restrict__ Dt = D + qb;
+        const int ln = tid & 63, wv = tid >> 6;
+        if (m_len > 0) {
+            uint32_t k = (uint32_t)__popcll(nzb & ((1ull << ln) - 1ull));
+            for (int i = 0; i < wv; ++i) k += s_wnz[i];
+            s_ksrc[k] = m_src - m_st;
+            atomicOr(&s_sbm[m_st >> 6], 1ull << (m_st & 63));
+        }
+        __syncthreads();
+        const uint32_t c = (uint32_t)__popcll(s_sbm[ln]);
+        const uint32_t pre = wave_scan_dpp(c) - c;  // set bits in the words below word ln
+        const uint32_t* __restrict__ St = stg.s + g0;
+        const uint32_t* __restrict__ Dt = stg.d + g0;
         for (uint32_t q0 = tid; q0 < ne; q0 += kU * kLprRows) {
             uint32_t sv[kU], dv[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                const uint32_t q = q0 + u * kLprRows;
-                sv[u] = q < ne ? St[q] : 0u;
-                dv[u] = q < ne ? Dt[q] : 0u;
+                const uint32_t q = std::min(q0 + u * kLprRows, ne - 1);
+                const uint32_t k = (uint32_t)__shfl((int)pre, (int)(q >> 6), 64) +
+                                   (uint32_t)__popcll(s_sbm[q >> 6] & (~0ull >> (63 - (q & 63)))) - 1u;
+                const uint32_t i = s_ksrc[k] + q;
+                sv[u] = q0 + u * kLprRows < ne ? St[i] : 0u;
+                dv[u] = q0 + u * kLprRows < ne ? Dt[i] : 0u;
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u)
@@ -1783,6 +1979,8 @@ struct Plan {
     uint32_t lpr_slot = 0;
     int64_t scan_blocks = 0;
     size_t lcnt = 0, loff = 0, lhl = 0, ltf = 0, lrow = 0, lcols = 0, lvals = 0;
+    size_t off2 = 0, gb = 0;  // staged runs (lpr_partition_kernel)
+    unsigned groups = 0;
 };
 
 constexpr unsigned kDeferCopyGrid = 32768;  // copy workgroups (grid-stride over the deferred list)
@@ -1852,9 +2050,11 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
                 pl.sb = sb;
                 pl.nb = std::max(nbk(sb), 1);
                 pl.ostride = (uint32_t)((pl.n_tiles + 31) & ~int64_t(31));
-                pl.te = pl.total;
-                pl.offt = pl.te + al(8 * (size_t)pl.n_tiles);
-                pl.s = pl.offt + al(2 * (size_t)(pl.nb + 1) * pl.ostride);
+                pl.groups = (unsigned)((pl.n_tiles + kRunGroup - 1) / kRunGroup);
+                pl.offt = pl.total;
+                pl.off2 = pl.offt + al(2 * (size_t)(pl.nb + 1) * pl.ostride);
+                pl.gb = pl.off2 + al(4 * (size_t)pl.nb * pl.ostride);
+                pl.s = pl.gb + al(8 * ((size_t)pl.groups * pl.nb + 1));
                 pl.d = pl.s + al(4 * (size_t)nnz_a);
                 pl.total = pl.d + al(4 * (size_t)nnz_a);
             }
@@ -1956,8 +2156,11 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
     return RP_OK;
 }
 
-size_t lpr_lds_bytes(int cap_a, size_t vs, uint32_t slot) {
-    return ((4 * (size_t)cap_a + 15) & ~size_t(15)) + ((8 * (size_t)slot + 15) & ~size_t(15)) + 4 * vs * (size_t)slot;
+size_t lpr_lds_bytes(int cap_a, size_t vs, uint32_t slot, bool staged) {
+    // staged: the slot buffers hold the run table (4 bytes per bucket + a 4096-bit map) in step A
+    const size_t bufs = std::max(((8 * (size_t)slot + 15) & ~size_t(15)) + 4 * vs * (size_t)slot,
+                                 staged ? (size_t)(4 * kStageMaxNB + 8 * 64) : (size_t)0);
+    return ((4 * (size_t)cap_a + 15) & ~size_t(15)) + bufs;
 }
 
 template <typename T, typename IP, typename OP, typename OI>
@@ -1972,41 +2175,50 @@ int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, con
     const unsigned n_tiles = (unsigned)pl.n_tiles;
     const IP* Ap = (const IP*)a->indptr;
     const T* Ax = (const T*)a->data;
-    const uint32_t *S = nullptr, *D = nullptr;
+    const unsigned t8 = (n_tiles + 7) / 8;
+    LprStage stg{};
     if (pl.staged) {
-        int64_t* TE = reinterpret_cast<int64_t*>(base + pl.te);
         uint16_t* OFFT = reinterpret_cast<uint16_t*>(base + pl.offt);
+        uint32_t* OFF2 = reinterpret_cast<uint32_t*>(base + pl.off2);
+        int64_t* GB = reinterpret_cast<int64_t*>(base + pl.gb);
         uint32_t* Sw = reinterpret_cast<uint32_t*>(base + pl.s);
         uint32_t* Dw = reinterpret_cast<uint32_t*>(base + pl.d);
-        const size_t plds = 4 * (size_t)pl.caps.cap_a;
-        HIP_TRY(hipFuncSetAttribute((const void*)stage_partition_kernel<T, IP>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(plds + sizeof(T) * pl.caps.cap_a)));
-        hipLaunchKernelGGL((stage_partition_kernel<T, IP>), dim3(n_tiles), dim3(kBlock), plds + sizeof(T) * pl.caps.cap_a,
-                           st, Ap, a->indices, Ax, a->n_rows, pl.caps, n_tiles, pl.sb, pl.nb, pl.ostride, Sw,
-                           (T*)nullptr, OFFT, TE);
+        hipLaunchKernelGGL((lpr_count_kernel<IP>), dim3(8 * t8), dim3(kBlock), 0, st, Ap, a->indices, a->n_rows,
+                           pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, OFFT);
         HIP_TRY(hipGetLastError());
-        const unsigned groups = (n_tiles + kGatherGroup - 1) / kGatherGroup;
-        const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * groups;
+        const unsigned nseg = pl.groups * (unsigned)pl.nb;
+        hipLaunchKernelGGL(lpr_run_scan_kernel, dim3(nseg), dim3(kBlock), 0, st, (const uint16_t*)OFFT, OFF2, GB,
+                           n_tiles, pl.nb, pl.ostride);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(lpr_seg_scan_kernel, dim3(1), dim3(1024), 0, st, GB, nseg);
+        HIP_TRY(hipGetLastError());
+        const size_t plds = 4 * (size_t)pl.caps.cap_a;
+        HIP_TRY(hipFuncSetAttribute((const void*)lpr_partition_kernel<IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)plds));
+        hipLaunchKernelGGL((lpr_partition_kernel<IP>), dim3(8 * t8), dim3(kBlock), plds, st, Ap, a->indices,
+                           a->n_rows, pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, (const uint16_t*)OFFT,
+                           (const uint32_t*)OFF2, (const int64_t*)GB, Sw);
+        HIP_TRY(hipGetLastError());
+        const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * pl.groups;
         const size_t glds = (size_t)4 << (pl.sb - 5);
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_gather_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds));
         hipLaunchKernelGGL(lpr_gather_kernel, dim3(grid), dim3(kGBlock), glds, st, (const uint32_t*)h->W32.p,
-                           (const uint32_t*)h->BM.p, (const int64_t*)TE, n_tiles, pl.sb, pl.nb, pl.ostride, groups,
-                           (const uint16_t*)OFFT, (const uint32_t*)Sw, Dw);
+                           (const uint32_t*)h->BM.p, (const int64_t*)GB, pl.sb, pl.nb, pl.groups,
+                           (const uint32_t*)Sw, Dw);
         HIP_TRY(hipGetLastError());
-        S = Sw;
-        D = Dw;
+        stg = LprStage{OFFT, OFF2, GB, Sw, Dw, pl.ostride, pl.nb};
     }
-    const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot);
+    const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot, pl.staged);
     if (pl.staged) {
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_main_kernel<T, IP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
-        hipLaunchKernelGGL((lpr_main_kernel<T, IP, true>), dim3(n_tiles), dim3(kLprRows), lds, st, R, mag, a->n_rows,
-                           Ap, a->indices, Ax, S, D, pl.caps.cap_a, n_tiles, order, sp, ws);
+        hipLaunchKernelGGL((lpr_main_kernel<T, IP, true>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag, a->n_rows,
+                           Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
     } else {
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_main_kernel<T, IP, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)lds));
-        hipLaunchKernelGGL((lpr_main_kernel<T, IP, false>), dim3(n_tiles), dim3(kLprRows), lds, st, R, mag, a->n_rows,
-                           Ap, a->indices, Ax, S, D, pl.caps.cap_a, n_tiles, order, sp, ws);
+        hipLaunchKernelGGL((lpr_main_kernel<T, IP, false>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag, a->n_rows,
+                           Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
     }
     HIP_TRY(hipGetLastError());
     const size_t hl = heavy_lds_bytes(h->p, sizeof(T));
@@ -2131,7 +2343,7 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
             plan = make_plan(h, a->n_rows, nnz_a_hint, false, vs, false);
     }
     const Caps& caps = plan.caps;
-    const size_t lds = plan.lpr ? std::max(lpr_lds_bytes(caps.cap_a, (size_t)vs, plan.lpr_slot), heavy_lds_bytes(h->p, (size_t)vs))
+    const size_t lds = plan.lpr ? std::max(lpr_lds_bytes(caps.cap_a, (size_t)vs, plan.lpr_slot, plan.staged), heavy_lds_bytes(h->p, (size_t)vs))
                                 : lds_bytes_for(caps, dtype_size(a->data_type), h->p);
     if (lds > 160 * 1024 - 4096)
         return fail(RP_ERR_UNSUPPORTED, "p=%lld too large for the LDS accumulator (%zu bytes)",

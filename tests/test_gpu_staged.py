@@ -148,3 +148,23 @@ def test_deferred_output_time_budget(R2m, ticks, monkeypatch):
                    kdd_like(rng, 25_000, m, powerlaw=True, values="normal")]).tocsr()
     want = oracle_product(A, R2m)
     assert_same_csr(Projector(R2m).matmul(A), *want)
+
+
+@pytest.mark.parametrize("pipe", ["tile", "lpr"])
+def test_pipelines_multi_group_vs_oracle(R2m, pipe, monkeypatch):
+    """Each pipeline forced (RP_PIPE), direct and staged, over 600k rows: 2344 row-lane tiles, so
+    the staged gather spans three 1024-tile groups and ends in a partial one; uniform and
+    power-law rows, empty rows, both orders."""
+    monkeypatch.setenv("RP_PIPE", pipe)
+    rng = np.random.default_rng(77)
+    m = R2m.shape[0]
+    A = sp.vstack([kdd_like(rng, 300_000, m, values="normal"), sp.csr_matrix((777, m), dtype=np.float32),
+                   kdd_like(rng, 299_223, m, powerlaw=True, values="normal")]).tocsr()
+    want = oracle_product(A, R2m)
+    Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
+    for stage in ("off", "on"):
+        P = Projector(R2m)
+        P.set_staging(stage, 19)
+        assert_same_csr(P.matmul(A), *want)
+        assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
+        P.close()
