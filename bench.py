@@ -374,6 +374,8 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax):
     rows = np.sort(rng.choice(n, size=min(4096, n), replace=False))
     A = sp.csr_matrix((ax, aj, ap), shape=(n, args.m))[rows]
     Wp, Wj, Wx, _, _ = smmp.matmat(A, R_host)
+    if order == "sorted":
+        Wj, Wx = smmp.sorted_rows(Wp, Wj, Wx)
     C = sp.csr_matrix((cx, cj, cp), shape=(n, args.p))[rows]
     same = (np.array_equal(C.indptr, Wp) and np.array_equal(C.indices, Wj)
             and np.array_equal(C.data.view(np.uint32), Wx.view(np.uint32)))
@@ -405,7 +407,8 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax):
 def verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host, n_sample=4096):
     """After the timed region: Cp monotone from 0 to nnz, every column in [0, p), and a seeded
     sample of rows (spread over the whole matrix) equal to the oracle's restatement of scipy's
-    csr_matmat, bit for bit (indices in scipy's per-row order and value bits)."""
+    csr_matmat, bit for bit (indices in scipy's per-row order, or ascending for --order sorted, and
+    value bits)."""
     import scipy.sparse as sp
     import torch
 
@@ -428,6 +431,8 @@ def verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host, n_sample=4096):
     ptr = np.concatenate([[0], np.cumsum(s1 - s0)])
     A = sp.csr_matrix((take(Ax, s0, s1), take(Aj, s0, s1), ptr), shape=(rows.size, args.m))
     Wp, Wj, Wx, _, _ = smmp.matmat(A, R_host)
+    if args.order == "sorted":
+        Wj, Wx = smmp.sorted_rows(Wp, Wj, Wx)
     got_ptr = np.concatenate([[0], np.cumsum(c1 - c0)])
     same = (np.array_equal(got_ptr, Wp) and np.array_equal(take(Cj, c0, c1), Wj)
             and np.array_equal(take(Cx, c0, c1).view(np.uint32), Wx.view(np.uint32)))

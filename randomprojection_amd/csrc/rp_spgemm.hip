@@ -192,6 +192,17 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// inclusive wave scan with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15/31)
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+
 // exclusive scan of one value per thread; *total = block sum. Contains two barriers.
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wsum, uint32_t* total) {
     const uint32_t inc = wave_incl_scan(v);
@@ -1101,7 +1112,7 @@ lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int64_t f = f0 + u * kGBlock;
-            v[u] = f >= lo && f < hi ? S[f] : 0u;
+            v[u] = f >= lo && f < hi ? __builtin_nontemporal_load(S + f) : 0u;  // streamed: keep the slice in L2
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -1113,7 +1124,7 @@ lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int64_t f = f0 + u * kGBlock;
-            if (f >= lo && f < hi) D[f] = v[u];
+            if (f >= lo && f < hi) __builtin_nontemporal_store(v[u], D + f);
         }
     }
 }
@@ -1216,16 +1227,6 @@ __device__ __forceinline__ T wave_incl_scan_t(T v, int lane) {
     return v;
 }
 
-// inclusive wave scan with DPP (row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15/31)
-__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
-    return v;
-}
 
 // staged runs of the row-lane pipeline (see lpr_partition_kernel)
 struct LprStage {
@@ -1268,6 +1269,12 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     const int nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
     const int64_t ea = (int64_t)Ap[row0];
     const int64_t ne64 = (int64_t)Ap[row0 + nrows] - ea;
+    // this wave's entry range [E0, E1) (wave-uniform) and the row pointers, all in the first round
+    const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t E0 = (uint32_t)((int64_t)Ap[row0 + std::min(64 * wu, nrows)] - ea);
+    const uint32_t E1 = (uint32_t)((int64_t)Ap[row0 + std::min(64 * wu + 64, nrows)] - ea);
+    const int64_t rp0 = tid <= nrows ? (int64_t)Ap[row0 + tid] : 0;
+    const int64_t rp1 = tid == 0 && nrows == kLprRows ? (int64_t)Ap[row0 + kLprRows] : 0;
     if (tid == 0) {
         s_nside = 0;
         s_bad = ne64 > cap_a;
@@ -1306,9 +1313,16 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     }
     STAMP(0);
     const uint32_t ne = (uint32_t)ne64;
-    // row pointers in flight together with step A's loads (stored to LDS after them)
-    const int64_t rp0 = tid <= nrows ? (int64_t)Ap[row0 + tid] : 0;
-    const int64_t rp1 = tid == 0 && nrows == kLprRows ? (int64_t)Ap[row0 + kLprRows] : 0;
+    // the flat pass's first values (entry order, coalesced) in flight together with step A's loads;
+    // unconditional loads (index clamped, value masked): straight-line vmcnt accounting
+    const T* __restrict__ Axw = Ax + ea;
+    const uint32_t elast = E1 > E0 ? E1 - 1 : E0;
+    auto ldx = [&](uint32_t j) {
+        const uint32_t e = E0 + 64 * j + (tid & 63);
+        const T v = Axw[std::min(e, elast)];
+        return e < E1 ? v : T(0);
+    };
+    T x0 = ldx(0), x1 = ldx(1), x2 = ldx(2), x3 = ldx(3);
     // ---- step A: R descriptors of the tile's entries into LDS, by entry
     // LDS descriptor of an entry: n <= 2 -> the W32 form (count, two inline 15-bit slots);
     // more entries -> code 3 | count (4 bits) << 26 | side index: the feature's W word lands in
@@ -1396,8 +1410,6 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     const int r = tid;  // this lane's row (for per-row work)
     const bool valid = r < nrows;
     const uint32_t rs = valid ? s_rowptr[r] : 0u, re = valid ? s_rowptr[r + 1] : 0u;
-    const int rlast = std::min(64 * w + 64, nrows);
-    const uint32_t E0 = s_rowptr[std::min(64 * w, nrows)], E1 = s_rowptr[rlast];
     const uint32_t nsteps = (E1 - E0 + 63) >> 6;
     for (uint32_t k = lane; k < nsteps; k += 64) s_flag[w][k] = 0ull;
     if (lane == 0) s_susp[w] = 0ull;
@@ -1415,7 +1427,6 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     // vmcnt accounting keeps the value prefetch in flight
     uint16_t* cb = s_colbuf + (size_t)w * sp.slot;
     T* vb = s_valbuf + (size_t)w * sp.slot;
-    const T* __restrict__ Axw = Ax + ea;
     uint32_t carry_r = 0, carry_k = 0;
     const T nmag = -mag;
     auto step = [&](uint32_t j, T x) {
@@ -1455,14 +1466,6 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         carry_r += (uint32_t)__builtin_popcountll(fw);
     };
     // values straight from HBM in entry order (coalesced), four steps in flight ahead of use
-    // unconditional loads (index clamped, value masked): straight-line vmcnt accounting
-    const uint32_t elast = E1 > E0 ? E1 - 1 : E0;
-    auto ldx = [&](uint32_t j) {
-        const uint32_t e = E0 + 64 * j + lane;
-        const T v = Axw[std::min(e, elast)];
-        return e < E1 ? v : T(0);
-    };
-    T x0 = ldx(0), x1 = ldx(1), x2 = ldx(2), x3 = ldx(3);
     for (uint32_t j = 0; j < nsteps; j += 4) {
         T c0 = x0, c1 = x1, c2 = x2, c3 = x3;
         x0 = ldx(j + 4);

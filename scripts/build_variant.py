@@ -1,0 +1,15 @@
+"""Build librp from a source variant into another file (A/B measurements with RP_LIB=<file>):
+    python scripts/build_variant.py <variant.hip> <out.so>
+The variant replaces csrc/rp_spgemm.hip; rp_libsvm.hip is shared."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from randomprojection_amd.build import FLAGS, HIPCC, SRC  # noqa: E402
+
+src = [sys.argv[1]] + [s for s in SRC if not s.endswith("rp_spgemm.hip")]
+inc = ["-I", os.path.join(ROOT, "randomprojection_amd", "csrc"), "-I", os.path.join(ROOT, "include")]
+subprocess.run([HIPCC, *FLAGS, *inc, "-o", sys.argv[2], *src], check=True)
+print(sys.argv[2])
