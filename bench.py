@@ -58,6 +58,32 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _src_sha16():
+    import hashlib
+
+    h = hashlib.sha256()
+    for n in ("rp_spgemm.hip", "rp_common.h"):
+        with open(os.path.join(ROOT, "randomprojection_amd", "csrc", n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+SRC_SHA16 = _src_sha16()  # keys profiles/*traffic*.json to the kernels they were measured on
+
+
+def step_kernels(plan):
+    """The kernels one rp_project_device call launches for this plan (rp_spgemm.hip)."""
+    if plan["pipeline"] == "rowlane":
+        ks = ["lpr_main_kernel", "lpr_heavy_count_kernel", "lpr_scan_kernel", "lpr_copy_kernel",
+              "lpr_heavy_write_kernel"]
+        if plan["staged"]:
+            ks = ["lpr_count_kernel", "lpr_run_scan_kernel", "lpr_seg_scan_kernel", "lpr_partition_kernel",
+                  "lpr_gather_kernel"] + ks
+        return ks
+    ks = ["spgemm_lookback_kernel", "defer_copy_kernel"]
+    return (["stage_partition_kernel", "stage_gather_kernel"] + ks) if plan["staged"] else ks
+
+
 def algorithmic_bytes_per_row(a, rbar, c):
     """Gustavson no-reuse model on the reference's formats (f32 values, int32
     indices, int32 row pointers): A ptr + idx/val, R ptr pair + gathered entries, C ptr + idx/val."""
@@ -198,6 +224,9 @@ def main():
             Cp = torch.empty(args.rows + 1, dtype=torch.int64, device=dev)
         nnz_c = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=args.order, stream=stream, workspace=ws, nnz_a=nnz_a)
 
+    plan = P.plan(args.rows, nnz_a)
+    log(f"[rank {rank}] pipeline: {plan}")
+
     def step():
         P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=args.order, stream=stream, workspace=ws, nnz_a=nnz_a, sync=False)
 
@@ -240,10 +269,10 @@ def main():
     # bit), and CSR well-formedness of the whole result on the device
     check = verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host) if rank == 0 else None
 
-    # rocprofv3 PMC results of an earlier profiling session of this same workload (profiles/):
-    # HBM bytes per step and the L2 hit rate of the main kernel (= on the R gathers, which are
-    # >90% of its reads); the explicit --traffic-json first, then any profiles/*traffic*.json (all
-    # profiled in direct mode: none applies to a staged run)
+    # rocprofv3 PMC results of a profiling session of this same workload on THIS build (profiles/):
+    # HBM bytes per step and the L2 hit rate of the main kernel. A traffic file applies only when
+    # it names the same rows, column distribution, pipeline and librp source hash: a kernel change
+    # without a fresh profile reports traffic null, never an old number.
     traffic, l2_hit, traffic_file = None, None, None
     cands = [args.traffic_json] + sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
     for f in cands:
@@ -251,7 +280,8 @@ def main():
             tj = json.load(open(f))
         except Exception:  # noqa: BLE001
             continue
-        if tj.get("rows") == args.rows and tj.get("dist") == args.dist and args.staging != "on":
+        if (tj.get("rows") == args.rows and tj.get("dist") == args.dist and tj.get("src_sha16") == SRC_SHA16
+                and tj.get("pipeline") == plan["pipeline"] and bool(tj.get("staged")) == plan["staged"]):
             traffic, l2_hit = tj.get("hbm_bytes_per_launch"), tj.get("l2_hit_rate_main_kernel")
             traffic_file = os.path.relpath(f, ROOT)
             break
@@ -284,9 +314,8 @@ def main():
                          "model": "B_row=(4+8a)+a(8+8r)+(4+8c)", "a": a, "r": rbar, "c": c,
                          "traffic_source": f"rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per step, {traffic_file}",
                          "l2_hit_rate_r_gathers": l2_hit,
-                         "step_kernels": ["spgemm_lookback_kernel", "defer_copy_kernel"] +
-                                         (["stage_partition_kernel", "stage_gather_kernel"]
-                                          if args.staging == "on" else []),
+                         "pipeline": plan, "librp_src_sha16": SRC_SHA16,
+                         "step_kernels": step_kernels(plan),
                          "traffic_GBps": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
                          "random_line_ceiling_G_per_s": RANDOM_LINE_CEILING / 1e9,
                          "gathers_G_per_s": gathers_per_s / 1e9,

@@ -154,6 +154,15 @@ int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_
  * bucket_shift: 2^shift features per bucket (0 = auto, 19). Results are identical either way. */
 int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift);
 
+/* The kernel pipeline rp_project_device would run for n_rows rows holding nnz_a entries with the
+ * full workspace: *pipeline = RP_PIPE_TILE (one-launch tile SpGEMM with look-back) or
+ * RP_PIPE_ROWLANE (row-lane kernel: short rows over a packed R), *staged = 1 if the R descriptors
+ * are fetched by the staged gather, *bucket_shift its bucket width (log2 features). Any out
+ * pointer may be NULL. For logging and benchmarks; results are identical on every pipeline. */
+typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1 } rp_pipeline;
+int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t* pipeline, int32_t* staged,
+                    int32_t* bucket_shift);
+
 /* C = A @ R, all device memory, enqueued on `stream` (hipStream_t, NULL = default).
  * workspace: caller device memory of workspace_bytes (>= rp_project_workspace_bytes(h, n, -1);
  * the full rp_project_workspace_bytes(h, n, nnz) also enables deferred tile output (no tile

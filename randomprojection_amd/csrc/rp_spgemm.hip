@@ -1356,7 +1356,10 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         const uint32_t pre = wave_scan_dpp(c) - c;  // set bits in the words below word ln
         const uint32_t* __restrict__ St = stg.s + g0;
         const uint32_t* __restrict__ Dt = stg.d + g0;
-        for (uint32_t q0 = tid; q0 < ne; q0 += kU * kLprRows) {
+        // block-uniform trip count: every lane of a wave takes part in the shuffle (a lane that had
+        // left the loop would hand back an undefined `pre` to the lanes still in it)
+        for (uint32_t b0 = 0; b0 < ne; b0 += kU * kLprRows) {
+            const uint32_t q0 = b0 + tid;
             uint32_t sv[kU], dv[kU];
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
@@ -1679,10 +1682,12 @@ lpr_heavy_write_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ 
 }
 
 // exclusive scan of the wave counts: 4096 per block (16 per thread), decoupled look-back over
-// blocks (taken in order from a ticket so every predecessor is running or done)
+// blocks (taken in order from a ticket so every predecessor is running or done). Offsets start at
+// *base_in (the entries of earlier row chunks); the running total goes to *base_out and ws->total.
 constexpr int kScanPer = 16;
 __global__ void __launch_bounds__(kBlock)
-lpr_scan_kernel(LprSpace sp, size_t n, unsigned long long base, Workspace* ws, unsigned* ticket) {
+lpr_scan_kernel(LprSpace sp, size_t n, const unsigned long long* __restrict__ base_in,
+                unsigned long long* __restrict__ base_out, Workspace* ws, unsigned* ticket) {
     __shared__ uint32_t s_wsum[kBlock / 64];
     __shared__ unsigned s_blk;
     __shared__ unsigned long long s_off;
@@ -1701,7 +1706,7 @@ lpr_scan_kernel(LprSpace sp, size_t n, unsigned long long base, Workspace* ws, u
     const uint32_t ex = block_excl_scan(local, s_wsum, &tot);
     if (threadIdx.x < 64) {
         const unsigned long long g = lookback_wave(sp.scan_state, blk, tot, ws);
-        if (threadIdx.x == 0) s_off = g + base;
+        if (threadIdx.x == 0) s_off = g + *base_in;
     }
     __syncthreads();
     unsigned long long o = s_off + ex;
@@ -1710,7 +1715,10 @@ lpr_scan_kernel(LprSpace sp, size_t n, unsigned long long base, Workspace* ws, u
         if (t0 + i < n) sp.off[t0 + i] = o;
         o += v[i];
     }
-    if (t0 < n && t0 + kScanPer >= n) ws->total = o - base;  // the thread holding the last count
+    if (t0 < n && t0 + kScanPer >= n) {  // the thread holding the last count: the running total
+        ws->total = o;
+        *base_out = o;
+    }
 }
 
 // slots -> C: one workgroup per tile (grid-stride), one wave per 64-row slot; rows reversed for
@@ -1980,6 +1988,9 @@ struct Plan {
     // row-lane pipeline (lpr_*): tiles of kLprRows rows, every tile's output in a fixed slot
     bool lpr = false;
     uint32_t lpr_slot = 0;
+    int64_t lpr_chunk = 0;    // rows per launch sequence (a multiple of kLprRows; n_rows if one)
+    size_t carry = 0;         // two u64 running-total slots (chunk k reads k & 1, writes the other)
+    size_t zero = 0;          // bytes zeroed once per call (header + states [+ carry])
     int64_t scan_blocks = 0;
     size_t lcnt = 0, loff = 0, lhl = 0, ltf = 0, lrow = 0, lcols = 0, lvals = 0;
     size_t off2 = 0, gb = 0;  // staged runs (lpr_partition_kernel)
@@ -1997,8 +2008,16 @@ constexpr int64_t kStageMinTable = 64ll << 20;  // ... and only a W past L2/MALL
 // Row-lane pipeline choice: packed R, short rows (one lane walks a row), few products per row.
 // RP_PIPE=tile|lpr forces a pipeline where it can run (tests, measurements).
 constexpr double kLprMaxRowEntries = 24.0, kLprMaxRowProducts = 24.0;
-constexpr bool kLprAuto = false;       // auto picks the row-lane pipeline (off until it measures faster)
-constexpr bool kLprStageAuto = false;  // ... and staging inside it
+constexpr bool kLprAuto = true;        // auto picks the row-lane pipeline (configs[1]: 22 ms vs 28 tile)
+constexpr bool kLprStageAuto = true;   // ... and staging inside it (large launches over a large R)
+// rows per launch sequence of the row-lane pipeline: the workspace (~150 B per KDD2012 row) is sized
+// for one chunk, so a launch of 1.08B rows (configs[2] on one GPU) needs ~20 GB, not ~190 GB
+constexpr int64_t kLprChunkRows = (int64_t)1 << 27;
+int64_t lpr_chunk_rows() {  // RP_LPR_CHUNK_ROWS (tests): smaller chunks, rounded up to whole tiles
+    if (const char* e = getenv("RP_LPR_CHUNK_ROWS"))
+        return std::max<int64_t>(kLprRows, (atoll(e) + kLprRows - 1) / kLprRows * kLprRows);
+    return kLprChunkRows;
+}
 bool lpr_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
     if (h->layout != RP_LAYOUT_PACKED || n_rows <= 0 || nnz_a < 0) return false;
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
@@ -2029,13 +2048,16 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
         // mean + 7 sigma (sigma ~ 1.25 sqrt(mean) for single-magnitude SRP rows) + 32: KDD2012 608,
         // which keeps a tile's LDS (descriptors + the 4 slots) at 32 KB: 5 tiles per CU
         pl.lpr_slot = (uint32_t)std::min<double>(65535.0, ((int)(prods_w + 8.75 * std::sqrt(prods_w) + 32.0) + 31) & ~31);
-        pl.n_tiles = (n_rows + kLprRows - 1) / kLprRows;
+        pl.lpr_chunk = std::min<int64_t>(n_rows, lpr_chunk_rows());
+        pl.n_tiles = (pl.lpr_chunk + kLprRows - 1) / kLprRows;
         const size_t nw = 4 * (size_t)pl.n_tiles;
         pl.scan_blocks = ((int64_t)nw + kBlock * kScanPer - 1) / (kBlock * kScanPer);
         // header, scan states and the per-tile heavy flags are zeroed by one memset per call
         pl.ltf = al(sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(pl.scan_blocks, 1));
         pl.head = pl.ltf + al(4 * (size_t)pl.n_tiles);
-        pl.lcnt = pl.head;
+        pl.carry = pl.head;
+        pl.zero = pl.carry + 16;
+        pl.lcnt = pl.carry + 256;
         pl.loff = pl.lcnt + al(4 * nw);
         pl.lhl = pl.loff + al(8 * nw);
         pl.lrow = pl.lhl + al(4 * (size_t)pl.n_tiles);
@@ -2057,9 +2079,12 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
                 pl.offt = pl.total;
                 pl.off2 = pl.offt + al(2 * (size_t)(pl.nb + 1) * pl.ostride);
                 pl.gb = pl.off2 + al(4 * (size_t)pl.nb * pl.ostride);
+                // staged entries of one chunk: all of them, or (several chunks) at most cap_a per
+                // tile (a tile past the cap stages nothing)
+                const size_t sd = pl.lpr_chunk < n_rows ? (size_t)pl.n_tiles * (size_t)pl.caps.cap_a : (size_t)nnz_a;
                 pl.s = pl.gb + al(8 * ((size_t)pl.groups * pl.nb + 1));
-                pl.d = pl.s + al(4 * (size_t)nnz_a);
-                pl.total = pl.d + al(4 * (size_t)nnz_a);
+                pl.d = pl.s + al(4 * sd);
+                pl.total = pl.d + al(4 * sd);
             }
         }
         return pl;
@@ -2067,6 +2092,7 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
     pl.caps = choose_caps(n_rows, nnz_a >= 0 ? nnz_a : n_rows * 11, ppe);
     pl.n_tiles = n_rows > 0 ? (n_rows + pl.caps.rpt - 1) / pl.caps.rpt : 0;
     pl.head = al(sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(pl.n_tiles, 1));
+    pl.zero = pl.head;
     pl.total = pl.head;
     if (pl.n_tiles > 0 && allow_defer && nnz_a >= 0) {  // deferred-output list, headers, pool
         pl.defer = true;
@@ -2167,15 +2193,16 @@ size_t lpr_lds_bytes(int cap_a, size_t vs, uint32_t slot, bool staged) {
 }
 
 template <typename T, typename IP, typename OP, typename OI>
-int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
-               Workspace* ws, const Plan& pl, hipStream_t st) {
+int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
+                     Workspace* ws, const Plan& pl, hipStream_t st, int64_t chunk) {
     char* base = reinterpret_cast<char*>(ws);
+    unsigned long long* carry = reinterpret_cast<unsigned long long*>(base + pl.carry);
     LprSpace sp{reinterpret_cast<uint32_t*>(base + pl.lcnt), reinterpret_cast<unsigned long long*>(base + pl.loff),
                 reinterpret_cast<uint32_t*>(base + pl.lhl), reinterpret_cast<uint32_t*>(base + pl.ltf),
                 reinterpret_cast<uint32_t*>(base + pl.lrow), reinterpret_cast<uint16_t*>(base + pl.lcols),
                 reinterpret_cast<unsigned char*>(base + pl.lvals), reinterpret_cast<unsigned long long*>(ws + 1),
                 pl.lpr_slot};
-    const unsigned n_tiles = (unsigned)pl.n_tiles;
+    const unsigned n_tiles = (unsigned)((a->n_rows + kLprRows - 1) / kLprRows);
     const IP* Ap = (const IP*)a->indptr;
     const T* Ax = (const T*)a->data;
     const unsigned t8 = (n_tiles + 7) / 8;
@@ -2230,8 +2257,10 @@ int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, con
     hipLaunchKernelGGL((lpr_heavy_count_kernel<T, IP>), dim3(256), dim3(kBlock), hl, st, R, mag, a->n_rows, Ap,
                        a->indices, Ax, (int)h->p, sp, ws);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(lpr_scan_kernel, dim3((unsigned)pl.scan_blocks), dim3(kBlock), 0, st, sp, 4 * (size_t)n_tiles,
-                       0ull, ws, &ws->tile_counter);
+    const unsigned scan_blocks = (unsigned)((4 * (size_t)n_tiles + kBlock * kScanPer - 1) / (kBlock * kScanPer));
+    hipLaunchKernelGGL(lpr_scan_kernel, dim3(scan_blocks), dim3(kBlock), 0, st, sp, 4 * (size_t)n_tiles,
+                       (const unsigned long long*)(carry + (chunk & 1)), carry + ((chunk + 1) & 1), ws,
+                       &ws->tile_counter);
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL((lpr_copy_kernel<T, OP, OI>), dim3(std::min<unsigned>(n_tiles, 1u << 20)), dim3(kBlock), 0, st,
                        sp, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices, (T*)c->data,
@@ -2243,6 +2272,29 @@ int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, con
                        a->indices, Ax, (int)h->p, sp, ws, (OP*)c->indptr, (OI*)c->indices, (T*)c->data,
                        (unsigned long long)c->capacity, order);
     HIP_TRY(hipGetLastError());
+    return RP_OK;
+}
+
+// The row-lane pipeline over chunks of pl.lpr_chunk rows (one chunk unless the launch is huge):
+// chunk k sees the rows [k * chunk, ...) as its own CSR (indptr offset, entries indexed through it),
+// writes its indptr slice and its entries at the running total of the chunks before it (a device
+// carry slot), and re-zeroes the per-chunk header and states first. All on one stream, no sync.
+template <typename T, typename IP, typename OP, typename OI>
+int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
+               Workspace* ws, const Plan& pl, hipStream_t st) {
+    const int64_t n = a->n_rows, step = std::max<int64_t>(pl.lpr_chunk, 1);
+    int64_t k = 0;
+    for (int64_t r0 = 0; r0 < n; r0 += step, ++k) {
+        rp_csr_in sa = *a;
+        sa.n_rows = std::min(step, n - r0);
+        sa.indptr = (const IP*)a->indptr + r0;
+        sa.nnz = -1;
+        rp_csr_out sc = *c;
+        sc.indptr = (OP*)c->indptr + r0;
+        if (k > 0) HIP_TRY(hipMemsetAsync(ws, 0, pl.head, st));  // the carry slots follow the header
+        const int rc = launch_lpr_chunk<T, IP, OP, OI>(R, mag, h, &sa, &sc, order, ws, pl, st, k);
+        if (rc) return rc;
+    }
     return RP_OK;
 }
 
@@ -2360,7 +2412,7 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
         if (rc) return rc;
         ws = (Workspace*)h->ws.p;
     }
-    HIP_TRY(hipMemsetAsync(ws, 0, plan.head, st));  // header + look-back states only
+    HIP_TRY(hipMemsetAsync(ws, 0, plan.zero, st));  // header + look-back states only
     if (n_tiles == 0) {
         // empty A: indptr = [0]
         if (c->indptr_type == RP_I64) {
@@ -2731,6 +2783,16 @@ int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_
         return (int64_t)((sizeof(Workspace) + 8 * (size_t)tiles + 255) & ~size_t(255));
     }
     return (int64_t)make_plan(h, n_rows, nnz_a).total;
+}
+
+int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t* pipeline, int32_t* staged,
+                    int32_t* bucket_shift) {
+    if (!h || n_rows < 0) return fail(RP_ERR_INVALID, "NULL projector or n_rows < 0");
+    const Plan pl = make_plan(h, n_rows, nnz_a);
+    if (pipeline) *pipeline = pl.lpr ? RP_PIPE_ROWLANE : RP_PIPE_TILE;
+    if (staged) *staged = pl.staged ? 1 : 0;
+    if (bucket_shift) *bucket_shift = pl.staged ? pl.sb : 0;
+    return RP_OK;
 }
 
 int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift) {

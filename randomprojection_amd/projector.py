@@ -307,6 +307,15 @@ class Projector:
         """Device workspace for ``project_device`` on n_rows rows / nnz_a entries (staging included)."""
         return int(self._lib.rp_project_workspace_bytes(self._h, int(n_rows), int(nnz_a)))
 
+    def plan(self, n_rows: int, nnz_a: int = -1) -> dict:
+        """The kernel pipeline ``project_device`` runs for this shape with a full workspace
+        (rp_project_plan): {"pipeline": "tile"|"rowlane", "staged": bool, "bucket_shift": int}."""
+        pipe, st, sb = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        nat.check(self._lib.rp_project_plan(self._h, int(n_rows), int(nnz_a), ctypes.byref(pipe), ctypes.byref(st),
+                                            ctypes.byref(sb)))
+        return {"pipeline": "rowlane" if pipe.value == 1 else "tile", "staged": bool(st.value),
+                "bucket_shift": int(sb.value)}
+
     def set_staging(self, mode: str = "auto", bucket_shift: int = 0):
         """Staged gather: "auto", "off" or "on" (identical results)."""
         code = {"auto": -1, "off": 0, "on": 1}[mode]

@@ -1,7 +1,8 @@
 """Summarise a rocprofv3 session of bench.py (scripts/gpu_profile.sh) into profiles/.
 
-One projection step = the kernels of rp_project_device: spgemm_lookback_kernel (+ defer_copy_kernel,
-+ stage_partition_kernel / stage_gather_kernel in staged mode). Reads
+One projection step = the kernels of rp_project_device: the row-lane pipeline (lpr_* kernels, the
+default for short rows over a packed R; staged: + count/run-scan/partition/gather) or the tile
+pipeline (spgemm_lookback_kernel + defer_copy_kernel, + stage_partition/stage_gather). Reads
 gpurun_out/prof_<tag>_trace/*kernel_stats.csv and the separate PMC passes
 (gpurun_out/prof_<tag>_pmc_*/*counter_collection.csv) and writes
   profiles/<tag>_kernel_stats.csv      the rocprofv3 --stats summary (copied)
@@ -23,7 +24,11 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel", "stage_partition_kernel", "stage_gather_kernel")
+STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel", "stage_partition_kernel", "stage_gather_kernel",
+                "lpr_count_kernel", "lpr_run_scan_kernel", "lpr_seg_scan_kernel", "lpr_partition_kernel",
+                "lpr_gather_kernel", "lpr_main_kernel", "lpr_heavy_count_kernel", "lpr_scan_kernel",
+                "lpr_copy_kernel", "lpr_heavy_write_kernel")
+MAIN_KERNELS = ("lpr_main_kernel", "spgemm_lookback_kernel")
 
 
 def short(name):
@@ -65,7 +70,16 @@ def main():
     ap.add_argument("--rows", type=int, default=119_705_032)
     ap.add_argument("--dist", default="uniform")
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--bench-json", default=None, help="the bench.py line of the profiled command (pipeline, "
+                                                        "librp source hash)")
+    ap.add_argument("--no-latest", action="store_true", help="do not overwrite profiles/traffic_latest.json")
     args = ap.parse_args()
+    bench = {}
+    if args.bench_json:
+        for line in open(args.bench_json):
+            if line.startswith("{"):
+                bench = json.loads(line)
+    roof = bench.get("roofline", {})
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     summary = {"tag": args.tag, "rows": args.rows, "dist": args.dist, "kernels": {}}
@@ -90,14 +104,21 @@ def main():
     summary["step_ms"] = step_ms
     summary["step"] = derive(dict(step_c), step_ms)
     json.dump(summary, open(os.path.join(prof, f"{args.tag}_summary.json"), "w"), indent=1)
+    plan = roof.get("pipeline", {})
+    summary.update(pipeline=plan.get("pipeline"), staged=plan.get("staged"), src_sha16=roof.get("librp_src_sha16"))
+    main_k = next((k for k in MAIN_KERNELS if k in summary["kernels"]), None)
     if "hbm_bytes" in summary["step"]:
-        json.dump({"tag": args.tag, "rows": args.rows, "dist": args.dist,
-                   "hbm_bytes_per_launch": summary["step"]["hbm_bytes"],
-                   "l2_hit_rate_main_kernel": summary["kernels"].get("spgemm_lookback_kernel", {}).get("l2_hit_rate"),
-                   "l2_hit_rate_step": summary["step"].get("l2_hit_rate"),
-                   "note": "per projection step (all kernels of rp_project_device)",
-                   "source": f"profiles/{args.tag}_summary.json"},
-                  open(os.path.join(prof, "traffic_latest.json"), "w"), indent=1)
+        tj = {"tag": args.tag, "rows": args.rows, "dist": args.dist,
+              "pipeline": plan.get("pipeline"), "staged": plan.get("staged"), "src_sha16": roof.get("librp_src_sha16"),
+              "hbm_bytes_per_launch": summary["step"]["hbm_bytes"],
+              "main_kernel": main_k,
+              "l2_hit_rate_main_kernel": summary["kernels"].get(main_k, {}).get("l2_hit_rate"),
+              "l2_hit_rate_step": summary["step"].get("l2_hit_rate"),
+              "note": "per projection step (all kernels of rp_project_device)",
+              "source": f"profiles/{args.tag}_summary.json"}
+        json.dump(tj, open(os.path.join(prof, f"{args.tag}_traffic.json"), "w"), indent=1)
+        if not args.no_latest:
+            json.dump(tj, open(os.path.join(prof, "traffic_latest.json"), "w"), indent=1)
     print(json.dumps(summary, indent=1))
 
 

@@ -64,7 +64,7 @@ def project(P, Ap, Aj, Ax, order="scipy", slack=1.02):
 
 
 @pytest.mark.parametrize("dist", ["uniform", "powerlaw"])
-def test_configs1_full_size(kdd, dist):
+def test_configs1_full_size(kdd, dist, monkeypatch):
     import torch
 
     R, P = kdd
@@ -77,6 +77,22 @@ def test_configs1_full_size(kdd, dist):
         assert 5.3 < nnz / KDD_ROWS < 6.3
         check_csr_on_device(Cp, Cj, nnz, sm.KDD_P, sorted_rows=(order == "sorted"))
         assert check_rows_vs_oracle(rows, Ap, Aj, Ax, Cp, Cj, Cx, R, order=order) > 350_000
+        if order == "scipy":
+            # the whole output against the other pipeline (the tile kernel with direct gathers):
+            # every byte equal, so a rare tile shape mishandled by either one cannot hide between
+            # the sampled rows
+            assert P.plan(KDD_ROWS, Aj.numel()) == {"pipeline": "rowlane", "staged": True, "bucket_shift": 19}
+            monkeypatch.setenv("RP_PIPE", "tile")
+            P.set_staging("off")
+            Tp, Tj, Tx, tn = project(P, Ap, Aj, Ax, order=order)
+            monkeypatch.delenv("RP_PIPE")
+            P.set_staging("auto")
+            assert tn == nnz and bool(torch.equal(Tp, Cp))
+            for s in range(0, nnz, 1 << 28):
+                e = min(nnz, s + (1 << 28))
+                assert bool(torch.equal(Tj[s:e], Cj[s:e])) and bool(torch.equal(Tx[s:e].view(torch.int32),
+                                                                                Cx[s:e].view(torch.int32)))
+            del Tp, Tj, Tx
         if dist == "uniform" and order == "scipy":
             # the same rows as a host CSR through the chunked stream path (boundary 2): the whole
             # 119.7M-row result equals the device-resident one, every byte

@@ -17,6 +17,13 @@ def R2m():
     return sm.projection_operand(sm.sparse_random_matrix(4096, 2_000_000, random_state=123))
 
 
+@pytest.fixture(scope="module")
+def R2m_p1k():
+    """2M features -> 1024: 0.72 R entries per feature, so KDD-like rows (11 entries, 8 products)
+    qualify for the row-lane pipeline (<= 24 products per row); R2m's 2.9 per feature do not."""
+    return sm.projection_operand(sm.sparse_random_matrix(1024, 2_000_000, random_state=123))
+
+
 def _staged(R, shift, **kw):
     P = Projector(R, **kw)
     P.set_staging("on", shift)
@@ -151,20 +158,96 @@ def test_deferred_output_time_budget(R2m, ticks, monkeypatch):
 
 
 @pytest.mark.parametrize("pipe", ["tile", "lpr"])
-def test_pipelines_multi_group_vs_oracle(R2m, pipe, monkeypatch):
+def test_pipelines_multi_group_vs_oracle(R2m_p1k, pipe, monkeypatch):
     """Each pipeline forced (RP_PIPE), direct and staged, over 600k rows: 2344 row-lane tiles, so
     the staged gather spans three 1024-tile groups and ends in a partial one; uniform and
     power-law rows, empty rows, both orders."""
     monkeypatch.setenv("RP_PIPE", pipe)
     rng = np.random.default_rng(77)
-    m = R2m.shape[0]
+    R = R2m_p1k
+    m = R.shape[0]
     A = sp.vstack([kdd_like(rng, 300_000, m, values="normal"), sp.csr_matrix((777, m), dtype=np.float32),
                    kdd_like(rng, 299_223, m, powerlaw=True, values="normal")]).tocsr()
-    want = oracle_product(A, R2m)
+    want = oracle_product(A, R)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     for stage in ("off", "on"):
-        P = Projector(R2m)
+        P = Projector(R)
         P.set_staging(stage, 19)
+        assert P.plan(A.shape[0], A.nnz)["pipeline"] == ("rowlane" if pipe == "lpr" else "tile")
         assert_same_csr(P.matmul(A), *want)
         assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
         P.close()
+
+
+@pytest.mark.parametrize("chunk", ["256", "50000"])
+def test_rowlane_chunked_launch_vs_oracle(R2m_p1k, chunk, monkeypatch):
+    """The row-lane pipeline over several row chunks (RP_LPR_CHUNK_ROWS; huge launches such as
+    configs[2]'s 1.08B rows run in chunks of 2^27): every chunk writes its indptr slice and its
+    entries at the running total of the chunks before it. Ragged last chunk, empty rows at a chunk
+    boundary, heavy rows, direct and staged, both orders, int64 output indptr."""
+    monkeypatch.setenv("RP_PIPE", "lpr")
+    monkeypatch.setenv("RP_LPR_CHUNK_ROWS", chunk)
+    rng = np.random.default_rng(91)
+    R = R2m_p1k
+    m = R.shape[0]
+    n1 = 50_176 if chunk == "50000" else 1024
+    A = sp.vstack([kdd_like(rng, n1 - 300, m, values="normal"), sp.csr_matrix((600, m), dtype=np.float32),
+                   kdd_like(rng, 2, m, mean=3000, values="normal", cap=m),
+                   kdd_like(rng, 123_321 if chunk == "50000" else 3001, m, powerlaw=True, values="normal")]).tocsr()
+    want = oracle_product(A, R)
+    Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
+    for stage in ("off", "on"):
+        P = Projector(R)
+        P.set_staging(stage, 19)
+        assert P.plan(A.shape[0], A.nnz) == {"pipeline": "rowlane", "staged": stage == "on",
+                                             "bucket_shift": 19 if stage == "on" else 0}
+        assert_same_csr(P.matmul(A), *want)
+        assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
+        P.close()
+    _device_int64_indptr_vs_oracle(R, A, want)
+
+
+def _device_int64_indptr_vs_oracle(R, A, want):
+    import torch
+
+    P = Projector(R)
+    dev = torch.device("cuda", 0)
+    Ap = torch.as_tensor(A.indptr.astype(np.int64), device=dev)
+    Aj = torch.as_tensor(A.indices.astype(np.int32), device=dev)
+    Ax = torch.as_tensor(A.data, device=dev)
+    n, cap = A.shape[0], int(want[0][-1]) + 100
+    Cp = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    Cj = torch.empty(cap, dtype=torch.int64, device=dev)
+    Cx = torch.empty(cap, dtype=torch.float32, device=dev)
+    ws = torch.empty(P.workspace_bytes(n, A.nnz), dtype=torch.uint8, device=dev)
+    nnz = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, workspace=ws, nnz_a=A.nnz)
+    assert nnz == int(want[0][-1])
+    assert np.array_equal(Cp.cpu().numpy(), want[0].astype(np.int64))
+    assert np.array_equal(Cj[:nnz].cpu().numpy(), want[1].astype(np.int64))
+    assert np.array_equal(Cx[:nnz].cpu().numpy().view(np.uint32), want[2].view(np.uint32))
+    P.close()
+
+
+def test_rowlane_staged_tile_past_one_round(R2m_p1k, monkeypatch):
+    """A tile of 3088 entries (> 12 x 256 = one round of the staged descriptor fetch, <= the entry
+    cap): the second round runs with 16 of 256 lanes in range. Regression: the run lookup shuffled
+    from lanes that had left the loop (found on 500M-row runs: one tile in ~1M)."""
+    monkeypatch.setenv("RP_PIPE", "lpr")
+    rng = np.random.default_rng(3088)
+    R = R2m_p1k
+    m = R.shape[0]
+    k = np.full(256, 12)
+    k[:16] = 13
+    cols = [np.sort(rng.choice(m, size=int(x), replace=False)) for x in k]
+    heavy = sp.csr_matrix((rng.standard_normal(int(k.sum())).astype(np.float32), np.concatenate(cols),
+                           np.concatenate([[0], np.cumsum(k)])), shape=(256, m))
+    A = sp.vstack([kdd_like(rng, 17 * 256, m, values="normal"), heavy,
+                   kdd_like(rng, 22 * 256 + 77, m, values="normal")]).tocsr()
+    want = oracle_product(A, R)
+    Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
+    P = Projector(R)
+    P.set_staging("on", 16)
+    assert P.plan(A.shape[0], A.nnz)["staged"]
+    assert_same_csr(P.matmul(A), *want)
+    assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
+    P.close()
