@@ -33,7 +33,7 @@ RANDOM_LINE_CEILING = 55e9  # random 128-B line fills/s, measured (scripts/probe
 # BASELINE.json configs: [1] KDD2012 train on one GPU (the headline); [3] the power-law stress shape
 CONFIGS = {
     "kdd": {"rows": 119_705_032, "m": 54_686_452, "p": 4096, "dist": "uniform", "mean_extra": 10.0,
-            "cpu_sample_rows": 64_000_000,
+            "cpu_sample_rows": 32_000_000,
             "metric": "rows/sec projected (whole node), KDD2012 54.7M->4096 dims; achieved HBM GB/s",
             "workload": "configs[1]: KDD2012 train {rows} rows x {m} -> {p} per GPU, device-resident CSR in/out",
             "data": "synthetic KDD2012-shaped rows ({dist} columns, 1+Poisson(10) nnz/row, values 1.0), "
@@ -107,7 +107,8 @@ def main():
     ap.add_argument("--staging", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--stage-shift", type=int, default=0, help="2^shift features per staging bucket (0 = auto)")
     ap.add_argument("--cpu-sample-rows", type=int, default=None)
-    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-part-rows", type=int, default=100_000,
+                    help="rows per recipe partition (one per core) in the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--boundary", choices=["device", "host"], default="device",
                     help="device: inputs/outputs resident in HBM (the default line); host: host CSR in -> host "
@@ -470,36 +471,48 @@ def verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host, n_sample=4096):
 
 
 def cpu_baseline(args, Ap, Aj, Ax, R_host):
-    """The oracle's C restatement of scipy csr_matmat (maxnnz + matmat, unfused) on host threads over
-    the first rows of the same workload: SURVEY.md §8(d)(ii), kind "port"."""
-    from oracle import smmp
+    """the reference's CPU path timed on this box's host cores, on a bounded sample
+    of the same workload, in a child process (oracle/cpu_baseline.py; this process holds the GPU,
+    the child forks one worker per core): (i) the recipe restated (oracle/recipe.py), one process
+    per core on partitions of part_rows rows -> `value`; (ii) scipy's kernel pair restated
+    (oracle/smmp.c) on N threads; each with a 1-core figure. kind "port": restatements (the
+    reference's own Python cannot travel to the box)."""
+    import subprocess
+    import tempfile
 
-    n = min(args.cpu_sample_rows, args.rows)
+    part = args.cpu_part_rows
+    krows = min(args.cpu_sample_rows, args.rows)
+    n = max(krows, part * 64)
+    n = min(n, args.rows)
     ap = Ap[: n + 1].cpu().numpy().astype(np.int64)
     e = int(ap[-1])
-    aj = Aj[:e].cpu().numpy()
-    ax = Ax[:e].cpu().numpy()
-    ap32 = (ap - ap[0]).astype(np.int32)
-    Bp = R_host.indptr.astype(np.int32)
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-    smmp.project_mt(ap32[:1001], aj, ax, Bp, R_host.indices, R_host.data, R_host.shape[1], 1)  # warm
-    t0 = time.perf_counter()
-    smmp.project_mt(ap32, aj, ax, Bp, R_host.indices, R_host.data, R_host.shape[1], threads)
-    dt = time.perf_counter() - t0
-    # context: scipy's own A @ R (the library call the reference makes, one core, the CSR operand
-    # already converted) on the first 1M of those rows
-    import scipy.sparse as sp
-
-    n1 = min(n, 1_000_000)
-    A1 = sp.csr_matrix((ax[:ap32[n1]], aj[:ap32[n1]], ap32[:n1 + 1]), shape=(n1, R_host.shape[0]))
-    t1 = time.perf_counter()
-    _ = A1 @ R_host
-    ds = time.perf_counter() - t1
-    return {"value": n / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} rows of the same synthetic workload; oracle/smmp.c (scipy csr_matmat_maxnnz + "
-                      f"csr_matmat restated) on {threads} threads, {dt:.2f}s wall",
-            "scipy_1core": {"value": n1 / ds, "unit": "rows/s", "rows": n1,
-                            "note": "scipy A @ R (csr_matmat), the reference's library call, 1 core"}}
+    base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else None
+    with tempfile.TemporaryDirectory(dir=base, prefix="rp_cpu_") as d:
+        np.save(os.path.join(d, "ap.npy"), (ap - ap[0]).astype(np.int64))
+        np.save(os.path.join(d, "aj.npy"), Aj[int(ap[0]):e].cpu().numpy())
+        np.save(os.path.join(d, "ax.npy"), Ax[int(ap[0]):e].cpu().numpy())
+        np.save(os.path.join(d, "rp.npy"), R_host.indptr.astype(np.int32))
+        np.save(os.path.join(d, "rj.npy"), R_host.indices.astype(np.int32))
+        np.save(os.path.join(d, "rx.npy"), R_host.data.astype(np.float32))
+        np.save(os.path.join(d, "p.npy"), np.int64(R_host.shape[1]))
+        env = dict(os.environ, PYTHONPATH=ROOT)
+        r = subprocess.run([sys.executable, "-m", "oracle.cpu_baseline", d, str(R_host.shape[0]), str(part),
+                            str(krows)], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        log(r.stderr[-2000:])
+        raise RuntimeError(f"cpu baseline child failed ({r.returncode})")
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    rec, ker = res["recipe"], res["kernel_port"]
+    return {"value": rec["value"], "unit": "rows/s", "cores": res["cores"], "kind": "port",
+            "sample": f"(i) the recipe restated (oracle/recipe.py: per-row COO->CSR, vstack, CSR @ CSC R, sorted "
+                      f"per-row SparseVector output), {rec['processes']} processes x {rec['part_rows']} rows of the "
+                      f"same synthetic workload, one partition each, started together",
+            "one_core": rec["one_core"],
+            "affinity_cpus": res["affinity_cpus"], "cgroup_quota_cpus": res["cgroup_quota_cpus"],
+            "recipe": rec,
+            "kernel_port": dict(ker, unit="rows/s",
+                                note="(ii) scipy csr_matmat_maxnnz + csr_matmat restated (oracle/smmp.c), first "
+                                     f"{ker['rows']} rows, {ker['threads']} threads")}
 
 
 if __name__ == "__main__":

@@ -19,6 +19,7 @@ import re
 import numpy as np
 
 _JDOUBLE = re.compile(r"^[+-]?(NaN|Infinity|((\d+\.?\d*|\.\d+)([eE][+-]?\d+)?)[fFdD]?)$")
+_JHEX = re.compile(r"^[+-]?0[xX]([0-9a-fA-F]+\.?|[0-9a-fA-F]*\.[0-9a-fA-F]+)[pP][+-]?\d+[fFdD]?$")
 _JINT = re.compile(r"^[+-]?\d+$")
 
 
@@ -40,6 +41,11 @@ def java_trim(s: str) -> str:
 
 def java_double(s: str) -> float:
     s = java_trim(s)
+    if _JHEX.match(s):  # HexFloatingPointLiteral (binary exponent required), correctly rounded
+        try:
+            return float.fromhex(s[:-1] if s[-1] in "fFdD" else s)
+        except OverflowError:  # rounds past the largest double: Java gives +-Infinity
+            return float("-inf") if s[0] == "-" else float("inf")
     if not _JDOUBLE.match(s):
         raise ValueError(s)
     if s[-1] in "fFdD" and "Infinity" not in s and "NaN" not in s:

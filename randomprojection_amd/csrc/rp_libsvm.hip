@@ -13,10 +13,12 @@
 // next (features.values.astype(np.float32), clustermode/randomProjection.py:38). Labels stay f64.
 //
 // Kernels: newline count/mark per 4 KiB block (16 B per lane loads), one thread per line for
-// tokenising/counting and for parsing (numbers by Clinger's exact fast path: <= 15 significant
-// digits and |exp10| <= 22, plus NaN/Infinity). A literal outside that path is reported, never
-// guessed (error code 7).
+// tokenising/counting and for parsing. Every literal Double.parseDouble accepts converts correctly
+// rounded: Clinger's fast path, Eisel-Lemire for any exponent, hex literals, and an exact
+// decimal-shifting slow path (slow_line_kernel) for the rare long literals the first two cannot
+// settle.
 #include "rp_common.h"
+#include "rp_pow5.h"
 
 #include <vector>
 
@@ -29,7 +31,7 @@ constexpr int kBytesPerThread = 16;
 constexpr int kBytesPerBlock = kLB * kBytesPerThread;
 
 enum : int {
-    E_LABEL = 1, E_INDEX = 2, E_NOVALUE = 3, E_VALUE = 4, E_ORDER = 5, E_RANGE = 6, E_LITERAL = 7
+    E_LABEL = 1, E_INDEX = 2, E_NOVALUE = 3, E_VALUE = 4, E_ORDER = 5, E_RANGE = 6
 };
 
 __device__ __forceinline__ bool is_ws(unsigned char c) { return c <= ' '; }  // Java String.trim
@@ -120,9 +122,121 @@ __global__ void line_count_kernel(const unsigned char* __restrict__ t, int64_t n
     }
 }
 
-// Java Double.parseDouble subset: [+-]? (digits [. digits?] | . digits) ([eE] [+-]? digits)?,
-// NaN, Infinity. Exact (correctly rounded) via Clinger's fast path; *ok = 0 for a syntax error,
-// 2 for a valid literal outside the exact path.
+// ---- decimal/hex text -> binary64, correctly rounded (Java Double.parseDouble, every literal):
+//   [+-]? (NaN | Infinity | digits [. digits?] | . digits) ([eE] [+-]? digits)? [fFdD]?
+//   [+-]? 0[xX] (hexdigits [.]? | hexdigits? . hexdigits) [pP] [+-]? digits [fFdD]?
+// Decimal literals with <= 19 significant digits: the Eisel-Lemire algorithm (Lemire 2021), exact
+// with no fallback for such mantissas (Mushtak & Lemire 2023). More digits: the first 19 give a
+// truncated mantissa w; if w and w + 1 round to the same double it is the answer, else the line is
+// handed to slow_line_kernel, which converts every digit exactly (decimal shifting, below).
+
+// m * 2^e2 correctly rounded to binary64 (round to nearest even); sticky: nonzero bits below m
+__device__ uint64_t round_bin64(uint64_t m, int e2, bool sticky) {
+    if (m == 0) return 0;
+    const int lz = __clzll(m);
+    m <<= lz;
+    e2 -= lz;
+    const int E = e2 + 63;  // exponent of the leading bit
+    if (E > 1023) return 0x7ff0000000000000ull;
+    const int shift = E >= -1022 ? 11 : 11 + (-1022 - E);
+    if (shift > 64) return 0;
+    const uint64_t kept = shift == 64 ? 0 : m >> shift;
+    const uint64_t rem = shift == 64 ? m : m << (64 - shift);  // dropped bits, top-aligned
+    const bool half = rem >> 63, rest = (rem << 1) != 0 || sticky;
+    uint64_t k = kept + ((half && (rest || (kept & 1))) ? 1 : 0);
+    if (E >= -1022) {
+        int Eo = E;
+        if (k == (1ull << 53)) {
+            k >>= 1;
+            ++Eo;
+            if (Eo > 1023) return 0x7ff0000000000000ull;
+        }
+        return ((uint64_t)(Eo + 1023) << 52) | (k & ((1ull << 52) - 1));
+    }
+    return k;  // subnormal (k == 2^52: the smallest normal, exponent field 1)
+}
+
+// Eisel-Lemire: w * 10^q (w != 0 exact) -> binary64 bits, no sign
+__device__ uint64_t eisel_lemire(int q, uint64_t w) {
+    if (q < kPow5Min) return 0;
+    if (q > kPow5Max) return 0x7ff0000000000000ull;
+    const int lz = __clzll(w);
+    w <<= lz;
+    const int idx = 2 * (q - kPow5Min);
+    uint64_t hi = __umul64hi(w, kPow5[idx]), lo = w * kPow5[idx];
+    constexpr uint64_t kPrecMask = 0xFFFFFFFFFFFFFFFFull >> 55;
+    if ((hi & kPrecMask) == kPrecMask) {
+        const uint64_t hi2 = __umul64hi(w, kPow5[idx + 1]);
+        lo += hi2;
+        if (hi2 > lo) ++hi;
+    }
+    const int upper = (int)(hi >> 63);
+    const int shift = upper + 64 - 52 - 3;
+    uint64_t mant = hi >> shift;
+    int p2 = (int)((((152170 + 65536) * (int64_t)q) >> 16) + 63) + upper - lz + 1023;
+    if (p2 <= 0) {  // subnormal
+        if (-p2 + 1 >= 64) return 0;
+        mant >>= -p2 + 1;
+        mant += mant & 1;
+        mant >>= 1;
+        return mant;  // mant == 2^52: the smallest normal
+    }
+    if (lo <= 1 && q >= -4 && q <= 23 && (mant & 3) == 1 && (mant << shift) == hi) mant &= ~1ull;
+    mant += mant & 1;
+    mant >>= 1;
+    if (mant >= (2ull << 52)) {
+        mant = 1ull << 52;
+        ++p2;
+    }
+    if (p2 >= 0x7ff) return 0x7ff0000000000000ull;
+    return ((uint64_t)p2 << 52) | (mant & ((1ull << 52) - 1));
+}
+
+__device__ __forceinline__ int hexval(unsigned char c) {
+    return c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+}
+
+// hex literal after "0x": value bits (no sign); *ok = 0 on a syntax error
+__device__ uint64_t parse_hex(const unsigned char* p, const unsigned char* end, int* ok) {
+    uint64_t m = 0;
+    int e2 = 0, nd = 0;
+    bool sticky = false, seen_nz = false;
+    auto digit = [&](int v, bool frac) {
+        ++nd;
+        if (!seen_nz && v == 0) {
+            if (frac) e2 -= 4;
+            return;
+        }
+        seen_nz = true;
+        if (m >> 60) {  // 64 bits kept: the rest only rounds
+            sticky |= v != 0;
+            if (!frac) e2 += 4;
+        } else {
+            m = (m << 4) | (uint64_t)v;
+            if (frac) e2 -= 4;
+        }
+    };
+    while (p < end && hexval(*p) >= 0) digit(hexval(*p++), false);
+    if (p < end && *p == '.') {
+        ++p;
+        while (p < end && hexval(*p) >= 0) digit(hexval(*p++), true);
+    }
+    if (nd == 0 || p >= end || (*p != 'p' && *p != 'P')) { *ok = 0; return 0; }
+    ++p;
+    bool eneg = false;
+    if (p < end && (*p == '+' || *p == '-')) { eneg = *p == '-'; ++p; }
+    if (p >= end || *p < '0' || *p > '9') { *ok = 0; return 0; }
+    int ev = 0;
+    while (p < end && *p >= '0' && *p <= '9') { ev = ev < 100000 ? ev * 10 + (*p - '0') : ev; ++p; }
+    if (p < end && (*p == 'f' || *p == 'F' || *p == 'd' || *p == 'D')) ++p;
+    if (p != end) { *ok = 0; return 0; }
+    *ok = 1;
+    if (m == 0) return 0;
+    const int64_t e = (int64_t)e2 + (eneg ? -ev : ev);
+    return round_bin64(m, (int)std::max<int64_t>(std::min<int64_t>(e, 4000), -4000), sticky);
+}
+
+// *ok: 1 parsed, 0 syntax error, 3 valid but needs the exact slow path (slow_line_kernel)
 __device__ double parse_double(const unsigned char* p, const unsigned char* end, int* ok) {
     *ok = 1;
     bool neg = false;
@@ -130,12 +244,18 @@ __device__ double parse_double(const unsigned char* p, const unsigned char* end,
         neg = *p == '-';
         ++p;
     }
+    const uint64_t sgn = neg ? 0x8000000000000000ull : 0ull;
     if (end - p == 3 && p[0] == 'N' && p[1] == 'a' && p[2] == 'N') return __longlong_as_double(0x7ff8000000000000ll);
     if (end - p == 8 && p[0] == 'I' && p[1] == 'n' && p[2] == 'f' && p[3] == 'i' && p[4] == 'n' &&
         p[5] == 'i' && p[6] == 't' && p[7] == 'y')
-        return neg ? -__longlong_as_double(0x7ff0000000000000ll) : __longlong_as_double(0x7ff0000000000000ll);
+        return __longlong_as_double((long long)(sgn | 0x7ff0000000000000ull));
+    if (end - p >= 2 && p[0] == '0' && (p[1] == 'x' || p[1] == 'X')) {
+        const uint64_t b = parse_hex(p + 2, end, ok);
+        return __longlong_as_double((long long)(sgn | b));
+    }
     uint64_t mant = 0;
-    int sig = 0, exp10 = 0, nd = 0;
+    int sig = 0, nd = 0;
+    int64_t exp10 = 0;
     bool lost = false;
     while (p < end && *p >= '0' && *p <= '9') {
         const int d = *p - '0';
@@ -164,30 +284,196 @@ __device__ double parse_double(const unsigned char* p, const unsigned char* end,
         bool eneg = false;
         if (p < end && (*p == '+' || *p == '-')) { eneg = *p == '-'; ++p; }
         if (p >= end || *p < '0' || *p > '9') { *ok = 0; return 0.0; }
-        int ev = 0;
+        int64_t ev = 0;
         while (p < end && *p >= '0' && *p <= '9') { ev = ev < 100000 ? ev * 10 + (*p - '0') : ev; ++p; }
         exp10 += eneg ? -ev : ev;
     }
-    if (p != end) {  // trailing characters: type suffix [fFdD] is valid Java but outside this path
-        *ok = (end - p == 1 && (*p == 'f' || *p == 'F' || *p == 'd' || *p == 'D')) ? 2 : 0;
-        return 0.0;
+    if (p < end && (*p == 'f' || *p == 'F' || *p == 'd' || *p == 'D')) ++p;  // Java type suffix
+    if (p != end) { *ok = 0; return 0.0; }
+    if (mant == 0) return __longlong_as_double((long long)sgn);
+    const int q = (int)std::max<int64_t>(std::min<int64_t>(exp10, 100000), -100000);
+    uint64_t b;
+    if (!lost && mant <= (1ull << 53) && q >= -22 && q <= 22) {  // Clinger: one exact operation
+        const double pw[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                               1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+        const double v = q >= 0 ? __dmul_rn((double)mant, pw[q]) : __ddiv_rn((double)mant, pw[-q]);
+        b = (uint64_t)__double_as_longlong(v);
+    } else {
+        b = eisel_lemire(q, mant);
+        if (lost && eisel_lemire(q, mant + 1) != b) {  // the dropped digits decide: exact path
+            *ok = 3;
+            return 0.0;
+        }
     }
-    if (mant == 0) return neg ? -0.0 : 0.0;
-    while (mant % 10 == 0) {  // 1e21 written out in full is still exact
-        mant /= 10;
-        ++exp10;
+    return __longlong_as_double((long long)(sgn | b));
+}
+
+// ---- exact slow path: the literal as a decimal digit string (up to kDecDigits significant digits,
+// `trunc` if nonzero digits were dropped), scaled by powers of two until it lies in [1/2, 1), then
+// 53 bits extracted with round-half-even (the classic decimal-shifting conversion).
+constexpr int kDecDigits = 800;
+struct Dec {
+    uint8_t d[kDecDigits + 24];
+    int nd, dp;
+    bool trunc;
+};
+
+__device__ void dec_trim(Dec& a) {
+    while (a.nd > 0 && a.d[a.nd - 1] == 0) --a.nd;
+    if (a.nd == 0) a.dp = 0;
+}
+
+__device__ void dec_rshift(Dec& a, int k) {  // a /= 2^k, k <= 60
+    int r = 0, w = 0;
+    uint64_t n = 0;
+    for (; (n >> k) == 0; ++r) {
+        if (r >= a.nd) {
+            if (n == 0) { a.nd = 0; return; }
+            while ((n >> k) == 0) { n *= 10; ++r; }
+            break;
+        }
+        n = n * 10 + a.d[r];
     }
-    // Clinger's extended fast path: move surplus powers of ten into the mantissa while it stays exact
-    while (exp10 > 22 && mant <= (1ull << 53) / 10) {
-        mant *= 10;
-        --exp10;
+    a.dp -= r - 1;
+    const uint64_t mask = (1ull << k) - 1;
+    for (; r < a.nd; ++r) {
+        const uint64_t c = a.d[r];
+        const uint64_t dig = n >> k;
+        n &= mask;
+        a.d[w++] = (uint8_t)dig;
+        n = n * 10 + c;
     }
-    if (lost || mant > (1ull << 53) || exp10 < -22 || exp10 > 22) { *ok = 2; return 0.0; }
-    const double pw[23] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
-                           1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-    double v = (double)mant;  // exact: mant <= 2^53
-    v = exp10 >= 0 ? __dmul_rn(v, pw[exp10]) : __ddiv_rn(v, pw[-exp10]);
-    return neg ? -v : v;
+    while (n > 0) {
+        const uint64_t dig = n >> k;
+        n &= mask;
+        if (w < kDecDigits) a.d[w++] = (uint8_t)dig;
+        else if (dig > 0) a.trunc = true;
+        n *= 10;
+    }
+    a.nd = w;
+    dec_trim(a);
+}
+
+__device__ void dec_lshift(Dec& a, int k) {  // a *= 2^k, k <= 60: at most 19 new leading digits
+    constexpr int kGrow = 20;
+    int w = a.nd + kGrow;
+    uint64_t n = 0;
+    for (int r = a.nd - 1; r >= 0; --r) {
+        n += (uint64_t)a.d[r] << k;
+        const uint64_t quo = n / 10, rem = n - 10 * quo;
+        --w;
+        a.d[w] = (uint8_t)rem;
+        n = quo;
+    }
+    while (n > 0) {
+        const uint64_t quo = n / 10, rem = n - 10 * quo;
+        --w;
+        a.d[w] = (uint8_t)rem;
+        n = quo;
+    }
+    int nn = a.nd + kGrow - w;  // digits now in d[w, w + nn)
+    for (int i = 0; i < nn; ++i) a.d[i] = a.d[w + i];
+    a.dp += kGrow - w;
+    if (nn > kDecDigits) {
+        for (int i = kDecDigits; i < nn; ++i) a.trunc |= a.d[i] != 0;
+        nn = kDecDigits;
+    }
+    a.nd = nn;
+    dec_trim(a);
+}
+
+__device__ void dec_shift(Dec& a, int k) {
+    if (a.nd == 0) return;
+    while (k > 60) { dec_lshift(a, 60); k -= 60; }
+    if (k > 0) dec_lshift(a, k);
+    while (k < -60) { dec_rshift(a, 60); k += 60; }
+    if (k < 0) dec_rshift(a, -k);
+}
+
+__device__ bool dec_round_up(const Dec& a, int nd) {
+    if (nd < 0 || nd >= a.nd) return false;
+    if (a.d[nd] == 5 && nd + 1 == a.nd) {  // exactly half-way (unless digits were dropped)
+        if (a.trunc) return true;
+        return nd > 0 && (a.d[nd - 1] & 1);
+    }
+    return a.d[nd] >= 5;
+}
+
+__device__ uint64_t dec_to_bits(Dec& a) {
+    constexpr int kBias = -1023, kMant = 52;
+    const int powtab[9] = {1, 3, 6, 9, 13, 16, 19, 23, 26};
+    if (a.nd == 0 || a.dp < -330) return 0;
+    if (a.dp > 310) return 0x7ff0000000000000ull;
+    int exp = 0;
+    while (a.dp > 0) {
+        const int n = a.dp >= 9 ? 27 : powtab[a.dp];
+        dec_shift(a, -n);
+        exp += n;
+    }
+    while (a.dp < 0 || (a.dp == 0 && a.d[0] < 5)) {
+        const int n = -a.dp >= 9 ? 27 : powtab[-a.dp];
+        dec_shift(a, n);
+        exp -= n;
+    }
+    --exp;  // [1/2, 1) -> [1, 2)
+    if (exp < kBias + 1) {
+        const int n = kBias + 1 - exp;
+        dec_shift(a, -n);
+        exp += n;
+    }
+    if (exp - kBias >= 0x7ff) return 0x7ff0000000000000ull;
+    dec_shift(a, 1 + kMant);
+    uint64_t mant = 0;
+    {
+        int i = 0;
+        for (; i < a.dp && i < a.nd; ++i) mant = mant * 10 + a.d[i];
+        for (; i < a.dp; ++i) mant *= 10;
+        if (dec_round_up(a, a.dp)) ++mant;
+    }
+    if (mant == (2ull << kMant)) {
+        mant >>= 1;
+        ++exp;
+        if (exp - kBias >= 0x7ff) return 0x7ff0000000000000ull;
+    }
+    if (!(mant & (1ull << kMant))) exp = kBias;
+    return (mant & ((1ull << kMant) - 1)) | ((uint64_t)((exp - kBias) & 0x7ff) << kMant);
+}
+
+// the exact conversion of a decimal literal already validated by parse_double (ok == 3 there)
+__device__ double parse_double_exact(const unsigned char* p, const unsigned char* end) {
+    Dec a;
+    a.nd = 0;
+    a.dp = 0;
+    a.trunc = false;
+    bool neg = false;
+    if (p < end && (*p == '+' || *p == '-')) { neg = *p == '-'; ++p; }
+    bool saw_dot = false, saw_nz = false;
+    int64_t dp = 0;
+    for (; p < end; ++p) {
+        const unsigned char c = *p;
+        if (c == '.') { saw_dot = true; continue; }
+        if (c < '0' || c > '9') break;
+        if (!saw_nz && c == '0') {
+            if (saw_dot) --dp;
+            continue;
+        }
+        saw_nz = true;
+        if (a.nd < kDecDigits) a.d[a.nd++] = (uint8_t)(c - '0');
+        else a.trunc |= c != '0';
+        if (!saw_dot) ++dp;
+    }
+    if (p < end && (*p == 'e' || *p == 'E')) {
+        ++p;
+        bool eneg = false;
+        if (p < end && (*p == '+' || *p == '-')) { eneg = *p == '-'; ++p; }
+        int64_t ev = 0;
+        while (p < end && *p >= '0' && *p <= '9') { ev = ev < 100000 ? ev * 10 + (*p - '0') : ev; ++p; }
+        dp += eneg ? -ev : ev;
+    }
+    a.dp = (int)std::max<int64_t>(std::min<int64_t>(dp, 100000), -100000);
+    dec_trim(a);
+    const uint64_t b = dec_to_bits(a);
+    return __longlong_as_double((long long)((neg ? 0x8000000000000000ull : 0ull) | b));
 }
 
 // Java Integer.parseInt: [+-]? digits, int32 range
@@ -207,66 +493,111 @@ __device__ bool parse_int(const unsigned char* p, const unsigned char* end, int6
     return true;
 }
 
+// one line -> its row (label, indptr, entries). EXACT = false: a literal that needs the exact slow
+// path (ok == 3) is left for slow_line_kernel (*slow = true); EXACT = true converts it here.
+template <typename IP, bool EXACT>
+__device__ int parse_line(const unsigned char* __restrict__ t, int64_t n, const int64_t* __restrict__ nl_pos,
+                          int64_t n_nl, int64_t i, const int64_t* __restrict__ row_of,
+                          const int64_t* __restrict__ off_of, int64_t num_features, double* __restrict__ labels,
+                          IP* __restrict__ indptr, int32_t* __restrict__ indices, float* __restrict__ data,
+                          bool* slow) {
+    const int64_t row = row_of[i];
+    int64_t out = off_of[i];
+    int64_t s, e;
+    line_span(nl_pos, n_nl, n, i, s, e);
+    while (s < e && is_ws(t[s])) ++s;
+    while (e > s && is_ws(t[e - 1])) --e;
+    int code = 0;
+    auto number = [&](int64_t a, int64_t b, int* ok) {
+        double v = parse_double(t + a, t + b, ok);
+        if (*ok == 3) {
+            if (EXACT) {
+                v = parse_double_exact(t + a, t + b);
+                *ok = 1;
+            } else {
+                *slow = true;
+                *ok = 1;  // placeholder; the exact kernel rewrites the whole line
+            }
+        }
+        return v;
+    };
+    // label: first split(' ') item
+    int64_t q = s;
+    while (q < e && t[q] != ' ') ++q;
+    {
+        // Double.parseDouble trims the item itself
+        int64_t a = s, b = q;
+        while (a < b && is_ws(t[a])) ++a;
+        while (b > a && is_ws(t[b - 1])) --b;
+        int ok;
+        const double lab = number(a, b, &ok);
+        if (ok != 1) code = E_LABEL;
+        labels[row] = lab;
+    }
+    indptr[row] = (IP)out;
+    int64_t prev = -1;
+    while (code == 0 && q < e) {
+        while (q < e && t[q] == ' ') ++q;
+        if (q >= e) break;
+        int64_t a = q;
+        while (q < e && t[q] != ' ') ++q;
+        // item [a, q): split(':') -> parts[0] index, parts[1] value (further parts ignored)
+        int64_t c1 = a;
+        while (c1 < q && t[c1] != ':') ++c1;
+        int64_t c2 = c1 < q ? c1 + 1 : q;
+        while (c2 < q && t[c2] != ':') ++c2;
+        if (c1 >= q || c2 == c1 + 1) { code = E_NOVALUE; break; }
+        int64_t idx;
+        if (!parse_int(t + a, t + c1, &idx)) { code = E_INDEX; break; }
+        int64_t va = c1 + 1, vb = c2;
+        while (va < vb && is_ws(t[va])) ++va;
+        while (vb > va && is_ws(t[vb - 1])) --vb;
+        int ok;
+        const double v = number(va, vb, &ok);
+        if (ok != 1) { code = E_VALUE; break; }
+        const int64_t j = idx - 1;
+        if (j <= prev) { code = E_ORDER; break; }
+        if (j >= num_features) { code = E_RANGE; break; }
+        prev = j;
+        indices[out] = (int32_t)j;
+        data[out] = (float)v;  // double -> float32 rounding, as features.values.astype(np.float32)
+        ++out;
+    }
+    return code;
+}
+
 template <typename IP>
 __global__ void line_parse_kernel(const unsigned char* __restrict__ t, int64_t n,
                                   const int64_t* __restrict__ nl_pos, int64_t n_nl, int64_t n_lines,
                                   const int64_t* __restrict__ row_of, const int64_t* __restrict__ off_of,
                                   int64_t num_features, double* __restrict__ labels, IP* __restrict__ indptr,
                                   int32_t* __restrict__ indices, float* __restrict__ data,
-                                  unsigned long long* __restrict__ err) {
+                                  unsigned long long* __restrict__ err, unsigned long long* __restrict__ n_slow,
+                                  int64_t* __restrict__ slow_lines) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_lines;
          i += (int64_t)gridDim.x * blockDim.x) {
         if (row_of[i + 1] == row_of[i]) continue;  // blank or comment line
-        const int64_t row = row_of[i];
-        int64_t out = off_of[i];
-        int64_t s, e;
-        line_span(nl_pos, n_nl, n, i, s, e);
-        while (s < e && is_ws(t[s])) ++s;
-        while (e > s && is_ws(t[e - 1])) --e;
-        int code = 0;
-        // label: first split(' ') item
-        int64_t q = s;
-        while (q < e && t[q] != ' ') ++q;
-        {
-            // Double.parseDouble trims the item itself
-            int64_t a = s, b = q;
-            while (a < b && is_ws(t[a])) ++a;
-            while (b > a && is_ws(t[b - 1])) --b;
-            int ok;
-            const double lab = parse_double(t + a, t + b, &ok);
-            if (ok != 1) code = ok == 2 ? E_LITERAL : E_LABEL;
-            labels[row] = lab;
-        }
-        indptr[row] = (IP)out;
-        int64_t prev = -1;
-        while (code == 0 && q < e) {
-            while (q < e && t[q] == ' ') ++q;
-            if (q >= e) break;
-            int64_t a = q;
-            while (q < e && t[q] != ' ') ++q;
-            // item [a, q): split(':') -> parts[0] index, parts[1] value (further parts ignored)
-            int64_t c1 = a;
-            while (c1 < q && t[c1] != ':') ++c1;
-            int64_t c2 = c1 < q ? c1 + 1 : q;
-            while (c2 < q && t[c2] != ':') ++c2;
-            if (c1 >= q || c2 == c1 + 1) { code = E_NOVALUE; break; }
-            int64_t idx;
-            if (!parse_int(t + a, t + c1, &idx)) { code = E_INDEX; break; }
-            int64_t va = c1 + 1, vb = c2;
-            while (va < vb && is_ws(t[va])) ++va;
-            while (vb > va && is_ws(t[vb - 1])) --vb;
-            int ok;
-            const double v = parse_double(t + va, t + vb, &ok);
-            if (ok != 1) { code = ok == 2 ? E_LITERAL : E_VALUE; break; }
-            const int64_t j = idx - 1;
-            if (j <= prev) { code = E_ORDER; break; }
-            if (j >= num_features) { code = E_RANGE; break; }
-            prev = j;
-            indices[out] = (int32_t)j;
-            data[out] = (float)v;
-            ++out;
-        }
+        bool slow = false;
+        const int code = parse_line<IP, false>(t, n, nl_pos, n_nl, i, row_of, off_of, num_features, labels, indptr,
+                                               indices, data, &slow);
         if (code) atomicMin(err, ((unsigned long long)i << 8) | (unsigned long long)code);
+        else if (slow) slow_lines[atomicAdd(n_slow, 1ull)] = i;
+    }
+}
+
+// lines holding a literal the fast parser could not settle: parsed again, every literal exact
+template <typename IP>
+__global__ void slow_line_kernel(const unsigned char* __restrict__ t, int64_t n, const int64_t* __restrict__ nl_pos,
+                                 int64_t n_nl, const int64_t* __restrict__ row_of, const int64_t* __restrict__ off_of,
+                                 int64_t num_features, double* __restrict__ labels, IP* __restrict__ indptr,
+                                 int32_t* __restrict__ indices, float* __restrict__ data,
+                                 const unsigned long long* __restrict__ n_slow, const int64_t* __restrict__ slow_lines) {
+    const unsigned long long ns = *n_slow;
+    for (unsigned long long k = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; k < ns;
+         k += (unsigned long long)gridDim.x * blockDim.x) {
+        bool slow = false;
+        (void)parse_line<IP, true>(t, n, nl_pos, n_nl, slow_lines[k], row_of, off_of, num_features, labels, indptr,
+                                   indices, data, &slow);
     }
 }
 
@@ -278,7 +609,6 @@ const char* reason(int c) {
         case E_VALUE: return "feature value is not a number";
         case E_ORDER: return "indices should be one-based and in ascending order";
         case E_RANGE: return "feature index >= numFeatures";
-        case E_LITERAL: return "numeric literal outside the exact GPU parser (hex, type suffix, >15 digits or |exp| > 22)";
         default: return "parse error";
     }
 }
@@ -297,7 +627,7 @@ extern "C" int rp_libsvm_parse_device(int device, const char* text, int64_t n_by
     const unsigned char* t = (const unsigned char*)text;
     if (((uintptr_t)t & 15) != 0) return fail(RP_ERR_INVALID, "text must be 16-byte aligned");
     const int64_t nblk = std::max<int64_t>((n_bytes + kBytesPerBlock - 1) / kBytesPerBlock, 1);
-    DevBuf counts, tmp, nl, keep, items, errb;
+    DevBuf counts, tmp, nl, keep, items, errb, slow;
     int rc;
     if ((rc = counts.ensure(8 * (size_t)nblk, device))) return rc;
     hipLaunchKernelGGL(nl_count_kernel, dim3((unsigned)nblk), dim3(kLB), 0, st, t, n_bytes, (int64_t*)counts.p);
@@ -319,11 +649,12 @@ extern "C" int rp_libsvm_parse_device(int device, const char* text, int64_t n_by
         HIP_TRY(hipGetLastError());
     }
     if ((rc = keep.ensure(8 * (size_t)(n_lines + 1), device)) || (rc = items.ensure(8 * (size_t)(n_lines + 1), device)) ||
-        (rc = errb.ensure(8, device)))
+        (rc = errb.ensure(16, device)))
         return rc;
     HIP_TRY(hipMemsetAsync(keep.p, 0, 8, st));
     HIP_TRY(hipMemsetAsync(items.p, 0, 8, st));
     HIP_TRY(hipMemsetAsync(errb.p, 0xff, 8, st));
+    HIP_TRY(hipMemsetAsync((char*)errb.p + 8, 0, 8, st));  // lines for the exact slow path
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_lines + 255) / 256, 1), 65536);
     if (n_lines > 0) {
         hipLaunchKernelGGL(line_count_kernel, dim3(grid), dim3(256), 0, st, t, n_bytes, (const int64_t*)nl.p, n_nl,
@@ -345,14 +676,26 @@ extern "C" int rp_libsvm_parse_device(int device, const char* text, int64_t n_by
     if (indptr_type == RP_I32 && total >= ((int64_t)1 << 31))
         return fail(RP_ERR_UNSUPPORTED, "nnz %lld needs int64 indptr", (long long)total);
     if (n_lines > 0) {
-        if (indptr_type == RP_I64)
+        if ((rc = slow.ensure(8 * (size_t)n_lines, device))) return rc;
+        unsigned long long* ns = (unsigned long long*)errb.p + 1;
+        const unsigned sgrid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_lines + 255) / 256, 1), 1024);
+        if (indptr_type == RP_I64) {
             hipLaunchKernelGGL((line_parse_kernel<int64_t>), dim3(grid), dim3(256), 0, st, t, n_bytes,
                                (const int64_t*)nl.p, n_nl, n_lines, (const int64_t*)keep.p, (const int64_t*)items.p,
-                               num_features, labels, (int64_t*)indptr, indices, data, (unsigned long long*)errb.p);
-        else
+                               num_features, labels, (int64_t*)indptr, indices, data, (unsigned long long*)errb.p,
+                               ns, (int64_t*)slow.p);
+            hipLaunchKernelGGL((slow_line_kernel<int64_t>), dim3(sgrid), dim3(64), 0, st, t, n_bytes,
+                               (const int64_t*)nl.p, n_nl, (const int64_t*)keep.p, (const int64_t*)items.p,
+                               num_features, labels, (int64_t*)indptr, indices, data, ns, (const int64_t*)slow.p);
+        } else {
             hipLaunchKernelGGL((line_parse_kernel<int32_t>), dim3(grid), dim3(256), 0, st, t, n_bytes,
                                (const int64_t*)nl.p, n_nl, n_lines, (const int64_t*)keep.p, (const int64_t*)items.p,
-                               num_features, labels, (int32_t*)indptr, indices, data, (unsigned long long*)errb.p);
+                               num_features, labels, (int32_t*)indptr, indices, data, (unsigned long long*)errb.p,
+                               ns, (int64_t*)slow.p);
+            hipLaunchKernelGGL((slow_line_kernel<int32_t>), dim3(sgrid), dim3(64), 0, st, t, n_bytes,
+                               (const int64_t*)nl.p, n_nl, (const int64_t*)keep.p, (const int64_t*)items.p,
+                               num_features, labels, (int32_t*)indptr, indices, data, ns, (const int64_t*)slow.p);
+        }
         HIP_TRY(hipGetLastError());
     }
     // indptr[rows] = total

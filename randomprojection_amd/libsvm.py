@@ -22,7 +22,8 @@ import scipy.sparse as sp
 from . import _native as nat
 from . import hostmem
 
-__all__ = ["parse_device", "parse_bytes", "iter_chunks", "load_libsvm", "project_libsvm", "partition_ids"]
+__all__ = ["parse_device", "parse_bytes", "iter_chunks", "split_range", "load_libsvm", "project_libsvm",
+           "libsvm_to_parquet", "partition_ids"]
 
 DEFAULT_CHUNK = 256 << 20
 
@@ -98,15 +99,36 @@ def parse_bytes(buf, num_features: int, device: int = 0):
     return labels.cpu().numpy(), X
 
 
-def iter_chunks(path: str, chunk_bytes: int = DEFAULT_CHUNK, copy: bool = True):
+def split_range(mm, size: int, lo: int, hi: int):
+    """The byte range of the lines that START in [lo, hi) (Hadoop's line-record split rule, which
+    Spark's text sources follow): a line straddling ``lo`` belongs to the previous split, the line
+    straddling ``hi`` to this one. Splits of consecutive ranges cover every line exactly once."""
+    lo, hi = max(0, min(lo, size)), max(0, min(hi, size))
+
+    def line_start_at_or_after(b):
+        if b <= 0:
+            return 0
+        if b >= size:
+            return size
+        if mm[b - 1:b] == b"\n":
+            return b
+        nl = mm.find(b"\n", b)
+        return size if nl < 0 else nl + 1
+
+    return line_start_at_or_after(lo), line_start_at_or_after(hi)
+
+
+def iter_chunks(path: str, chunk_bytes: int = DEFAULT_CHUNK, copy: bool = True, byte_range=None):
     """Newline-aligned chunks of a file (memory-mapped, never loaded whole). ``copy=False`` yields
     memoryviews of the mapping instead of bytes: each is valid until the next chunk is requested
-    and must be released (``del``) by then."""
+    and must be released (``del``) by then. ``byte_range=(lo, hi)``: only the lines that start in
+    [lo, hi) (one rank's split of the file, see ``split_range``)."""
     size = os.path.getsize(path)
     if size == 0:
         return
     with open(path, "rb") as f, mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as mm:
-        start = 0
+        start, stop = (0, size) if byte_range is None else split_range(mm, size, *byte_range)
+        size = stop
         while start < size:
             end = min(start + chunk_bytes, size)
             if end < size:
@@ -134,14 +156,17 @@ def load_libsvm(path: str, num_features: int, chunk_bytes: int = DEFAULT_CHUNK, 
         yield partition_ids(ci, X.shape[0]), labels, X
 
 
-def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order: str = "sorted"):
+def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order: str = "sorted",
+                   byte_range=None, partition_base: int = 0):
     """libsvm text -> GPU parse -> GPU projection -> host CSR, per chunk: yields
-    ``(ids, labels, C)`` with ``C`` = the chunk's rows of ``X @ R`` (scipy CSR, float32)."""
+    ``(ids, labels, C)`` with ``C`` = the chunk's rows of ``X @ R`` (scipy CSR, float32).
+    ``byte_range``: only the lines starting in [lo, hi) (a rank's split); chunk k gets partition id
+    ``partition_base + k`` in its row ids."""
     import torch
 
     dev = projector.device
     st = torch.cuda.current_stream(torch.device("cuda", dev)).cuda_stream  # where torch fills/frees the tensors
-    for ci, buf in enumerate(iter_chunks(path, chunk_bytes, copy=False)):
+    for ci, buf in enumerate(iter_chunks(path, chunk_bytes, copy=False, byte_range=byte_range)):
         t, n = _to_device(buf, dev)
         del buf  # the view must be gone before the next chunk (the mapping closes at the end)
         labels, Ap, Aj, Ax = parse_device(t, n, projector.m, dev, stream=st)
@@ -162,7 +187,25 @@ def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order
         if k < 2**31:  # the index dtype scipy's csr_matrix settles on
             Cp = Cp.to(torch.int32)
         C = sp.csr_matrix((_download(Cx[:k]), _download(Cj[:k]), _download(Cp)), shape=(rows, projector.p))
-        yield partition_ids(ci, rows), _download(labels), C
+        yield partition_ids(partition_base + ci, rows), _download(labels), C
+
+
+def libsvm_to_parquet(path: str, projector, out_dir: str, chunk_bytes: int = DEFAULT_CHUNK, byte_range=None,
+                      partition_base: int = 0, compression: str = "snappy"):
+    """The recipe end to end for one rank: libsvm text -> GPU parse -> GPU projection -> one Parquet
+    part file per chunk (``part-<partition>.parquet``, schema (id Long, label Float, features
+    VectorUDT), code/clustermode/randomProjection.py:71-80,107-113). Returns the part file paths."""
+    from . import egress
+
+    os.makedirs(out_dir, exist_ok=True)
+    parts = []
+    for ids, labels, C in project_libsvm(path, projector, chunk_bytes, order="sorted", byte_range=byte_range,
+                                         partition_base=partition_base):
+        pid = int(ids[0] >> 33) if len(ids) else partition_base + len(parts)
+        f = os.path.join(out_dir, f"part-{pid:08d}.parquet")
+        egress.write_parquet(f, ids, labels, C, compression=compression)
+        parts.append(f)
+    return parts
 
 
 def _download(t):

@@ -105,3 +105,43 @@ def test_plan_shards_balanced_and_covering(world):
 def test_plan_shards_degenerate():
     assert list(plan_shards(np.zeros(5, np.int64), 2)) == [0, 2, 4]
     assert list(plan_shards(np.array([0]), 4)) == [0, 0, 0, 0, 0]
+
+
+def _lines_of(path, world, chunk_bytes):
+    from randomprojection_amd.libsvm import iter_chunks
+
+    size = os.path.getsize(path)
+    per_rank = []
+    for r in range(world):
+        got = b"".join(iter_chunks(path, chunk_bytes, byte_range=(size * r // world, size * (r + 1) // world)))
+        per_rank.append(got)
+    return per_rank
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("trailing_newline", [True, False])
+def test_rank_byte_splits_cover_every_line_once(tmp_path, world, trailing_newline):
+    """Each rank reads only the lines that START in its equal byte share (the split rule of
+    libsvm.split_range / ShardedProjector.byte_range): concatenated in rank order they are the file,
+    whatever the chunk size, with lines straddling every boundary."""
+    rng = np.random.default_rng(world)
+    lines = [("1" if i & 1 else "0") + "".join(f" {j}:1" for j in np.sort(rng.choice(10**6, int(rng.integers(0, 40)),
+                                                                                      replace=False)) + 1)
+             for i in range(500)]
+    text = "\n".join(lines) + ("\n" if trailing_newline else "")
+    path = tmp_path / "x.libsvm"
+    path.write_bytes(text.encode())
+    for chunk in (64, 1000, 1 << 20):
+        parts = _lines_of(str(path), world, chunk)
+        assert b"".join(parts) == text.encode()
+        # every rank's text is whole lines
+        for p in parts[:-1]:
+            assert p == b"" or p.endswith(b"\n")
+
+
+def test_partition_ids_unique_and_increasing_across_ranks():
+    from randomprojection_amd.driver import PARTITION_BITS_PER_RANK
+    from randomprojection_amd.libsvm import partition_ids
+
+    ids = np.concatenate([partition_ids((r << PARTITION_BITS_PER_RANK) + c, 1000) for r in range(8) for c in range(3)])
+    assert np.all(np.diff(ids) > 0)

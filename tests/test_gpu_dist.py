@@ -1,0 +1,92 @@
+"""ShardedProjector itself on the GPU with 2 ranks (child processes sharing cuda:0 over gloo):
+R built on rank 0 only and broadcast, each rank projecting only its own rows — a host shard, a
+device shard, and its byte split of a libsvm file written to Parquet part files — and the pieces
+assembling to the oracle's product of the whole matrix (code/clustermode/randomProjection.py:
+72,104,107-113)."""
+import glob
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import smmp
+from oracle.libsvm_ref import parse_text
+from randomprojection_amd import egress, srp_matrix as sm
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_sharded_projector_two_ranks(tmp_path):
+    world = 2
+    rng = np.random.default_rng(8)
+    m = 300_000
+    lines = []
+    for i in range(3000):
+        idx = np.sort(rng.choice(m, int(rng.integers(0, 20)), replace=False)) + 1
+        lines.append(f"{i % 2}" + "".join(f" {j}:{rng.standard_normal():.6g}" for j in idx))
+    text = ("\n".join(lines) + "\n").encode()
+    tp = tmp_path / "train.libsvm"
+    tp.write_bytes(text)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world))
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_gpu_worker.py"), str(tmp_path), str(tp)],
+                              env=dict(env, RANK=str(r), LOCAL_RANK="0"), stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=240)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert all(p.returncode == 0 for p in procs), "\n".join(o[-3000:] for o in outs)
+    res = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    A = sp.csr_matrix((res[0]["A_data"], res[0]["A_indices"], res[0]["A_indptr"]), shape=(res[0]["A_indptr"].size - 1, m))
+    R = sm.projection_operand(sm.sparse_random_matrix(256, m, random_state=123))
+    Wp, Wj, Wx, _, _ = smmp.matmat(A, R)
+    for pre in ("", "d_"):
+        gp, gj, gx = [0], [], []
+        for r in range(world):
+            z = res[r]
+            assert int(z[pre + "row" if pre else "row_off"]) == len(gp) - 1
+            assert int(z[pre + "nnz" if pre else "nnz_off"]) == len(gj)
+            ip = z[pre + "indptr"].astype(np.int64)
+            gp.extend((len(gj) + ip[1:] - ip[0]).tolist())
+            gj.extend(z[pre + "indices"].tolist())
+            gx.append(z[pre + "data"])
+        assert np.array_equal(np.array(gp), Wp) and np.array_equal(np.array(gj), Wj)
+        assert np.array_equal(np.concatenate(gx).view(np.uint32), Wx.view(np.uint32))
+    # libsvm splits: each rank's part files; together every line once, ids unique and increasing
+    assert res[0]["byte_range"][1] == res[1]["byte_range"][0]
+    files = sorted(glob.glob(str(tmp_path / "parquet" / "part-*.parquet")))
+    assert sorted(files) == sorted(str(f) for z in res for f in z["parts"])
+    ids, labels, Cs = [], [], []
+    for f in files:
+        i_, l_, c_ = egress.read_parquet(f)
+        ids.append(i_)
+        labels.append(l_)
+        Cs.append(c_)
+    ids = np.concatenate(ids)
+    assert np.all(np.diff(ids) > 0) and ids.size == 3000
+    assert (ids[-1] >> 33) >= (1 << 20)  # rank 1's partitions
+    lab, ip, ij, iv = parse_text(text, m)
+    X = sp.csr_matrix((iv, ij, ip), shape=(lab.size, m))
+    Xp, Xj, Xx, _, _ = smmp.matmat(X, R)
+    Xj, Xx = smmp.sorted_rows(Xp, Xj, Xx)
+    C = sp.vstack(Cs).tocsr()
+    assert np.array_equal(np.concatenate(labels), lab.astype(np.float32))
+    assert np.array_equal(C.indptr, Xp) and np.array_equal(C.indices, Xj)
+    assert np.array_equal(C.data, Xx.astype(np.float64))

@@ -90,3 +90,54 @@ def test_project_libsvm_end_to_end(tmp_path):
     assert same(np.concatenate(got_lab), lab)
     assert np.array_equal(C.indptr, Cp) and np.array_equal(C.indices, Cj_s) and same(C.data, Cx_s)
     assert all(int(i[0]) == (k << 33) for k, i in enumerate(got_ids))
+
+
+def _tricky_literals(rng):
+    """Literals outside Clinger's fast path: 17-digit shortest round trips, 20-40 digit values,
+    exact decimal expansions of half-way points between adjacent doubles (ties: round half even)
+    and their neighbours 1e-30 relative away (the exact slow path), |exp| > 22, subnormals,
+    overflow/underflow, hex literals and Java type suffixes."""
+    import decimal
+
+    decimal.getcontext().prec = 1200
+    out = []
+    for _ in range(300):
+        x = float(rng.standard_normal() * 10.0 ** rng.integers(-30, 30))
+        out.append(repr(x))
+        out.append(f"{x:.25e}")
+        out.append(f"{x:.40g}")
+    for _ in range(200):  # half-way points and near misses
+        x = abs(float(rng.standard_normal() * 10.0 ** rng.integers(-300, 300))) or 1.0
+        y = np.nextafter(x, np.inf)
+        h = (decimal.Decimal(x) + decimal.Decimal(y)) / 2
+        out.append(format(h, "f") if abs(h.adjusted()) < 30 else format(h, "e"))
+        for eps in ("1e-60", "-1e-60"):
+            v = h * (1 + decimal.Decimal(eps))
+            out.append(format(v, "e"))
+    for e in range(-330, -300):  # subnormals and the underflow edge
+        out.append(f"{rng.integers(1, 99999)}e{e}")
+        out.append(f"4.9e{e - 294}" if e == -330 else f"2.4703282292062327e-324")
+    out += ["1e400", "-1e400", "1e-400", "2.2250738585072011e-308", "2.2250738585072012e-308",
+            "1.7976931348623157e308", "1.7976931348623158e308", "1.7976931348623159e308",
+            "0x1.8p1", "-0x.1p-2", "0X1P-1074", "0x1.fffffffffffff8p1023", "0x1.000000000000081p0", "1.5f", "2d",
+            "123456789012345678901234567890", "0.1234567890123456789012345678901234567890e-5",
+            "9007199254740993", "9007199254740993.0000000000000000001", "1" + "0" * 400 + "e-400"]
+    return out
+
+
+def test_every_java_double_literal_exact():
+    """Every value Java's Double.parseDouble accepts, correctly rounded to binary64 (labels) and
+    then to float32 (features, the recipe's astype(np.float32)), against the restated parser."""
+    rng = np.random.default_rng(17)
+    lits = _tricky_literals(rng)
+    lines = []
+    for k in range(0, len(lits), 5):
+        chunk = lits[k:k + 5]
+        lines.append(chunk[0] + "".join(f" {i + 1}:{v}" for i, v in enumerate(chunk)))
+    txt = ("\n".join(lines) + "\n").encode()
+    lab, ip, ix, vx = parse_text(txt, 10)
+    labels, X = parse_bytes(txt, 10)
+    bad = np.nonzero(labels.view(np.uint64) != lab.view(np.uint64))[0]
+    assert bad.size == 0, [(lines[i].split()[0], labels[i], lab[i]) for i in bad[:5]]
+    assert np.array_equal(X.indptr, ip) and np.array_equal(X.indices, ix)
+    assert same(X.data, vx)

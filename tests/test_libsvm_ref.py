@@ -52,3 +52,14 @@ def test_chunker_aligns_on_newlines(tmp_path):
 def test_partition_ids():
     ids = partition_ids(3, 4)
     assert list(ids) == [(3 << 33) + i for i in range(4)]
+
+
+def test_java_hex_and_suffix_literals():
+    from oracle.libsvm_ref import java_double
+
+    assert java_double("0x1.8p1") == 3.0 and java_double("-0x.1p-2f") == -0.015625
+    assert java_double("0X1P-1074") == 5e-324 and java_double("0x1.fffffffffffff8p1023") == float("inf")
+    assert java_double("1.5d") == 1.5 and java_double("1e400") == float("inf") and java_double("1e-400") == 0.0
+    for bad in ("0x1.8", "0x", "1.5g", "0x1p", "inf", "1_0"):
+        with pytest.raises(ValueError):
+            java_double(bad)
