@@ -69,7 +69,7 @@ typedef enum {
     RP_ERR_TIMEOUT = 6       /* a device-side bounded wait expired (should never happen) */
 } rp_status;
 
-typedef enum { RP_I32 = 1, RP_I64 = 2, RP_F32 = 3, RP_F64 = 4 } rp_dtype;
+typedef enum { RP_I32 = 1, RP_I64 = 2, RP_F32 = 3, RP_F64 = 4, RP_BF16 = 5 } rp_dtype;
 
 typedef enum {
     RP_LAYOUT_AUTO = 0,      /* packed when R has one magnitude and p <= 16384, else generic */
@@ -229,6 +229,14 @@ int rp_libsvm_parse_device(int device, const char* text, int64_t n_bytes, int64_
                            double* labels, void* indptr, int32_t indptr_type, int32_t* indices,
                            float* data, int64_t cap_rows, int64_t cap_nnz, void* stream,
                            int64_t* n_rows, int64_t* nnz, int64_t* err_line);
+
+/* Dense Gaussian projection (BASELINE configs[4]): Y[n x p] (f32, row stride ldy) = X[n x m] .
+ * G[p x m]^T for device arrays X and G of dtype RP_F32 (exact-f32 MFMA products, f32 accumulate) or
+ * RP_BF16 (bf16 operands, f32 accumulate), both row-major, 16-byte aligned, m a multiple of 32
+ * (f32) / 64 (bf16). Replaces sklearn GaussianRandomProjection.transform's X @ components_.T
+ * (sklearn/random_projection.py:569-612) with a hand-written MFMA GEMM. Asynchronous on `stream`. */
+int rp_dense_project_device(int device, const void* X, int32_t dtype, int64_t n, int64_t m, const void* G,
+                            int64_t p, float* Y, int64_t ldy, void* stream);
 
 #ifdef __cplusplus
 }

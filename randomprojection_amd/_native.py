@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(HERE, "librp.so")
 _LIB_OVERRIDE = os.environ.get("RP_LIB")
 
 RP_OK, RP_ERR_INVALID, RP_ERR_HIP, RP_ERR_CAPACITY, RP_ERR_UNSUPPORTED, RP_ERR_NOMEM, RP_ERR_TIMEOUT = range(7)
-RP_I32, RP_I64, RP_F32, RP_F64 = 1, 2, 3, 4
+RP_I32, RP_I64, RP_F32, RP_F64, RP_BF16 = 1, 2, 3, 4, 5
 RP_LAYOUT_AUTO, RP_LAYOUT_GENERIC, RP_LAYOUT_PACKED = 0, 1, 2
 RP_ORDER_SCIPY, RP_ORDER_SORTED = 0, 1
 
@@ -25,6 +25,7 @@ EXPORTS = (
     "rp_project_workspace_bytes", "rp_project_plan", "rp_projector_set_staging", "rp_project_device",
     "rp_project_host_begin", "rp_result_fetch", "rp_result_free", "rp_project",
     "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_project_stream", "rp_host_alloc", "rp_host_free",
+    "rp_dense_project_device",
 )
 
 
@@ -118,6 +119,7 @@ def load(path: str = None):
         "rp_host_free": (ctypes.c_int, [vp]),
         "rp_synth_rows_device": (ctypes.c_int, [ctypes.c_int, i64, i64, dbl, i32, i32, dbl, ctypes.c_uint64,
                                                 vp, i32, vp, vp, vp, P(i64)]),
+        "rp_dense_project_device": (ctypes.c_int, [ctypes.c_int, vp, i32, i64, i64, vp, i64, vp, i64, vp]),
         "rp_libsvm_parse_device": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, vp, vp, i32, vp, vp, i64, i64, vp,
                                                   P(i64), P(i64), P(i64)]),
     }

@@ -6,7 +6,7 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = [os.path.join(HERE, "csrc", n) for n in ("rp_spgemm.hip", "rp_libsvm.hip")]
+SRC = [os.path.join(HERE, "csrc", n) for n in ("rp_spgemm.hip", "rp_libsvm.hip", "rp_dense.hip")]
 OUT = os.path.join(HERE, "librp.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [
@@ -20,7 +20,8 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SRC + [os.path.join(HERE, "..", "include", "rp.h"), os.path.join(HERE, "csrc", "rp_common.h")]
+    deps = SRC + [os.path.join(HERE, "..", "include", "rp.h"), os.path.join(HERE, "csrc", "rp_common.h"),
+                  os.path.join(HERE, "csrc", "rp_pow5.h")]
     return any(os.path.getmtime(s) > t for s in deps)
 
 
