@@ -30,10 +30,24 @@ DIAG_OUT = os.path.join(HERE, "librp_diag.so")
 
 def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
     """librp.so; ``diag=True`` builds librp_diag.so instead (in-kernel stage stamps, -DRP_STAMPS),
-    used only by scripts/stage_stamps.py, never by the package."""
+    used only by scripts/stage_stamps.py, never by the package. Sources compile in parallel (one
+    hipcc per .hip into build/), then link."""
     out = DIAG_OUT if diag else OUT
     if force or diag or needs_build():
-        cmd = [HIPCC, *FLAGS, *(["-DRP_STAMPS"] if diag else []), "-o", out + ".tmp", *SRC]
+        extra = ["-DRP_STAMPS"] if diag else []
+        odir = os.path.join(HERE, "build", "diag" if diag else "rel")
+        os.makedirs(odir, exist_ok=True)
+        objs, procs = [], []
+        for src in SRC:
+            obj = os.path.join(odir, os.path.basename(src) + ".o")
+            cmd = [HIPCC, *[f for f in FLAGS if f != "-shared"], *extra, "-c", "-o", obj, src]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            objs.append(obj)
+            procs.append(subprocess.Popen(cmd))
+        if any(p.wait() != 0 for p in procs):
+            raise subprocess.CalledProcessError(1, "hipcc")
+        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

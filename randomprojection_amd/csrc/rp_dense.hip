@@ -25,9 +25,7 @@ using namespace rpd;
 
 namespace {
 
-constexpr int kDBM = 128, kDBN = 128, kDThreads = 256;
-constexpr int kRowBytes = 128;                       // one K step of a row
-constexpr int kTileBytes = kDBM * kRowBytes;         // 16 KB per operand per stage
+constexpr int kRowBytes = 128;  // one K step of a row (64 bf16 / 32 f32), 8 chunks of 16 B
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -41,23 +39,21 @@ struct DenseStep;
 template <>
 struct DenseStep<uint16_t> {
     static constexpr int kElems = 64;
-    __device__ static void compute(const uint4* __restrict__ sA, const uint4* __restrict__ sB, int wm, int wn,
-                                   int lane, f32x16 (&acc)[2][2]) {
+    template <int TM, int TN>
+    __device__ static void compute(const uint4* __restrict__ sA, const uint4* __restrict__ sB, int ra0, int rb0,
+                                   int lane, f32x16 (&acc)[TM][TN]) {
         const int r = lane & 31, h = lane >> 5;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            bf16x8 a[2], b[2];
+            bf16x8 a[TM], b[TN];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int ra = wm * 64 + i * 32 + r, rb = wn * 64 + i * 32 + r;
-                const uint4 va = sA[swz(ra, 2 * s + h)], vb = sB[swz(rb, 2 * s + h)];
-                a[i] = __builtin_bit_cast(bf16x8, va);
-                b[i] = __builtin_bit_cast(bf16x8, vb);
-            }
+            for (int i = 0; i < TM; ++i) a[i] = __builtin_bit_cast(bf16x8, sA[swz(ra0 + i * 32 + r, 2 * s + h)]);
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int j = 0; j < TN; ++j) b[j] = __builtin_bit_cast(bf16x8, sB[swz(rb0 + j * 32 + r, 2 * s + h)]);
 #pragma unroll
-                for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
         }
     }
@@ -68,111 +64,154 @@ struct DenseStep<uint16_t> {
 template <>
 struct DenseStep<float> {
     static constexpr int kElems = 32;
-    __device__ static void compute(const uint4* __restrict__ sA, const uint4* __restrict__ sB, int wm, int wn,
-                                   int lane, f32x16 (&acc)[2][2]) {
+    template <int TM, int TN>
+    __device__ static void compute(const uint4* __restrict__ sA, const uint4* __restrict__ sB, int ra0, int rb0,
+                                   int lane, f32x16 (&acc)[TM][TN]) {
         const int r = lane & 31, h = lane >> 5;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            float a[2][4], b[2][4];
+            uint4 a[TM], b[TN];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const int ra = wm * 64 + i * 32 + r, rb = wn * 64 + i * 32 + r;
-                const uint4 va = sA[swz(ra, 4 * h + q)], vb = sB[swz(rb, 4 * h + q)];
-                a[i][0] = __uint_as_float(va.x); a[i][1] = __uint_as_float(va.y);
-                a[i][2] = __uint_as_float(va.z); a[i][3] = __uint_as_float(va.w);
-                b[i][0] = __uint_as_float(vb.x); b[i][1] = __uint_as_float(vb.y);
-                b[i][2] = __uint_as_float(vb.z); b[i][3] = __uint_as_float(vb.w);
-            }
+            for (int i = 0; i < TM; ++i) a[i] = sA[swz(ra0 + i * 32 + r, 4 * h + q)];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) b[j] = sB[swz(rb0 + j * 32 + r, 4 * h + q)];
 #pragma unroll
             for (int e = 0; e < 4; ++e)
 #pragma unroll
-                for (int i = 0; i < 2; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], b[j][e], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < TN; ++j) {
+                        const uint32_t ua = e == 0 ? a[i].x : e == 1 ? a[i].y : e == 2 ? a[i].z : a[i].w;
+                        const uint32_t ub = e == 0 ? b[j].x : e == 1 ? b[j].y : e == 2 ? b[j].z : b[j].w;
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(ua), __uint_as_float(ub),
+                                                                         acc[i][j], 0, 0, 0);
+                    }
         }
     }
 };
 
-// One block: rows [m0, m0 + 128) of A x rows [n0, n0 + 128) of B. Rows past M / N are read as
-// zeros (clamped loads, masked) and not stored. K must be a multiple of the step (host check).
-template <typename T>
-__global__ void __launch_bounds__(kDThreads)
+// Block tile (WM*TM*32) x (WN*TN*32): WM x WN waves, each TM x TN MFMA tiles of 32 x 32. STAGES = 2:
+// two LDS buffers, the next step loaded to registers during the MFMAs and written to the other
+// buffer (one barrier per step); STAGES = 1: one buffer, written after a barrier (half the LDS,
+// so twice the blocks per CU). Rows past M / N are read as zeros and not stored.
+template <typename T, int WM, int WN, int TM, int TN, int STAGES>
+__global__ void __launch_bounds__(64 * WM * WN)
 dense_nt_kernel(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C, int64_t M, int N, int K,
                 int64_t ldc, unsigned m_tiles, unsigned n_tiles) {
-    __shared__ uint4 lds[2][2][kTileBytes / 16];  // [stage][A|B][128 rows x 8 chunks]: 64 KB
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32, NT = 64 * WM * WN;
+    constexpr int PA = BM * 8 / NT, PB = BN * 8 / NT;  // 16-B chunks per thread per step
+    static_assert(PA * NT == BM * 8 && PB * NT == BN * 8, "tile/threads");
+    __shared__ uint4 lds[STAGES][(BM + BN) * 8];
     // XCD-aware tile order (see the file header)
     const unsigned i = blockIdx.x, xcd = i & 7u, j = i >> 3;
     const unsigned mt = (j / n_tiles) * 8u + xcd, nt = j % n_tiles;
     if (mt >= m_tiles) return;  // uniform
-    const int64_t m0 = (int64_t)mt * kDBM;
-    const int n0 = (int)nt * kDBN;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+    const int64_t m0 = (int64_t)mt * BM;
+    const int n0 = (int)nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w / WN, wn = w % WN;
     constexpr int kE = DenseStep<T>::kElems;
     const int steps = K / kE;
-    // staging: thread t moves chunks t + 256 q (q < 4) of each operand: row (t >> 3) + 32 q, chunk t & 7
+    constexpr int RPP = NT / 8;  // rows covered by one pass of the block (8 chunks per row)
     const int srow = tid >> 3, sch = tid & 7;
-    const char* __restrict__ ga[4];
-    const char* __restrict__ gb[4];
-    bool va[4], vb[4];
+    const char* __restrict__ ga[PA];
+    const char* __restrict__ gb[PB];
+    bool va[PA], vb[PB];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int64_t ra = m0 + srow + 32 * q;
-        const int rb = n0 + srow + 32 * q;
+    for (int q = 0; q < PA; ++q) {
+        const int64_t ra = m0 + srow + RPP * q;
         va[q] = ra < M;
-        vb[q] = rb < N;
         ga[q] = reinterpret_cast<const char*>(A + (va[q] ? ra : 0) * (int64_t)K) + sch * 16;
+    }
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+        const int rb = n0 + srow + RPP * q;
+        vb[q] = rb < N;
         gb[q] = reinterpret_cast<const char*>(B + (int64_t)(vb[q] ? rb : 0) * K) + sch * 16;
     }
-    uint4 ra[4], rb[4];
+    uint4 ra[PA], rb[PB];
     auto load = [&](int s) {
         const int64_t off = (int64_t)s * kRowBytes;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ra[q] = *reinterpret_cast<const uint4*>(ga[q] + off);
-            rb[q] = *reinterpret_cast<const uint4*>(gb[q] + off);
-        }
+        for (int q = 0; q < PA; ++q) ra[q] = *reinterpret_cast<const uint4*>(ga[q] + off);
+#pragma unroll
+        for (int q = 0; q < PB; ++q) rb[q] = *reinterpret_cast<const uint4*>(gb[q] + off);
     };
     auto store = [&](int buf) {
+        const uint4 z = make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint4 z = make_uint4(0, 0, 0, 0);
-            lds[buf][0][swz(srow + 32 * q, sch)] = va[q] ? ra[q] : z;
-            lds[buf][1][swz(srow + 32 * q, sch)] = vb[q] ? rb[q] : z;
-        }
+        for (int q = 0; q < PA; ++q) lds[buf][swz(srow + RPP * q, sch)] = va[q] ? ra[q] : z;
+#pragma unroll
+        for (int q = 0; q < PB; ++q) lds[buf][BM * 8 + swz(srow + RPP * q, sch)] = vb[q] ? rb[q] : z;
     };
-    f32x16 acc[2][2];
+    f32x16 acc[TM][TN];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < TN; ++b)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+    const int ra0 = wm * TM * 32, rb0 = wn * TN * 32;
     load(0);
     store(0);
     __syncthreads();
     for (int s = 0; s < steps; ++s) {
-        const int cur = s & 1;
+        const int cur = STAGES == 2 ? (s & 1) : 0;
         if (s + 1 < steps) load(s + 1);  // in flight while this step's MFMAs run
-        DenseStep<T>::compute(lds[cur][0], lds[cur][1], wm, wn, lane, acc);
-        if (s + 1 < steps) store(cur ^ 1);  // the other buffer: last read before the previous barrier
-        __syncthreads();
+        DenseStep<T>::template compute<TM, TN>(lds[cur], lds[cur] + BM * 8, ra0, rb0, lane, acc);
+        if (STAGES == 2) {
+            if (s + 1 < steps) store(cur ^ 1);  // the other buffer: last read before the previous barrier
+            __syncthreads();
+        } else {
+            __syncthreads();
+            if (s + 1 < steps) store(0);
+            __syncthreads();
+        }
     }
-    // epilogue: 32 x 32 tile (i, j) of the wave; lane holds column lane & 31, rows
+    // epilogue: lane holds column lane & 31 of each 32 x 32 tile, rows
     // (e & 3) + 8 (e >> 2) + 4 (lane >> 5) for e < 16
     const int col = lane & 31, rh = 4 * (lane >> 5);
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int c = n0 + wn * 64 + b * 32 + col;
+        for (int b = 0; b < TN; ++b) {
+            const int c = n0 + rb0 + b * 32 + col;
             if (c >= N) continue;
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const int64_t r = m0 + wm * 64 + a * 32 + (e & 3) + 8 * (e >> 2) + rh;
+                const int64_t r = m0 + ra0 + a * 32 + (e & 3) + 8 * (e >> 2) + rh;
                 if (r < M) C[r * ldc + c] = acc[a][b][e];
             }
         }
+}
+
+template <typename T, int WM, int WN, int TM, int TN, int STAGES>
+int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
+                 hipStream_t st) {
+    constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
+    const unsigned m_tiles = (unsigned)((n + BM - 1) / BM), n_tiles = (unsigned)((p + BN - 1) / BN);
+    const uint64_t blocks = (uint64_t)((m_tiles + 7) / 8) * 8ull * n_tiles;
+    if (blocks >= (1ull << 31)) return fail(RP_ERR_UNSUPPORTED, "too many rows for one launch");
+    hipLaunchKernelGGL((dense_nt_kernel<T, WM, WN, TM, TN, STAGES>), dim3((unsigned)blocks), dim3(64 * WM * WN), 0,
+                       st, (const T*)X, (const T*)G, Y, n, (int)p, (int)m, ldy, m_tiles, n_tiles);
+    HIP_TRY(hipGetLastError());
+    return RP_OK;
+}
+
+// tile variants (RP_DENSE_VARIANT, measurements): 0 = 128x128 2 stages, 1 = 128x128 1 stage,
+// 2 = 256x128 1 stage, 3 = 128x256 2 stages (8 waves), 4 = 256x256 1 stage (8 waves), 5 = 256x256
+// 2 stages (128 KB LDS, 8 waves)
+constexpr int kDenseVariant = 0;
+template <typename T>
+int dispatch_dense(int v, const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
+                   hipStream_t st) {
+    switch (v) {
+        case 1: return launch_dense<T, 2, 2, 2, 2, 1>(X, G, Y, n, m, p, ldy, st);
+        case 2: return launch_dense<T, 2, 2, 4, 2, 1>(X, G, Y, n, m, p, ldy, st);
+        case 3: return launch_dense<T, 2, 4, 2, 2, 2>(X, G, Y, n, m, p, ldy, st);
+        case 4: return launch_dense<T, 2, 4, 4, 2, 1>(X, G, Y, n, m, p, ldy, st);
+        case 5: return launch_dense<T, 2, 4, 4, 2, 2>(X, G, Y, n, m, p, ldy, st);
+        default: return launch_dense<T, 2, 2, 2, 2, 2>(X, G, Y, n, m, p, ldy, st);
+    }
 }
 
 }  // namespace
@@ -189,16 +228,9 @@ extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype,
     if (al & 15) return fail(RP_ERR_INVALID, "X and G must be 16-byte aligned");
     if (n == 0) return RP_OK;
     HIP_TRY(hipSetDevice(device));
-    const unsigned m_tiles = (unsigned)((n + kDBM - 1) / kDBM), n_tiles = (unsigned)((p + kDBN - 1) / kDBN);
-    const uint64_t blocks = (uint64_t)((m_tiles + 7) / 8) * 8ull * n_tiles;
-    if (blocks >= (1ull << 31)) return fail(RP_ERR_UNSUPPORTED, "too many rows for one launch");
+    const char* e = getenv("RP_DENSE_VARIANT");
+    const int v = e ? atoi(e) : kDenseVariant;
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == RP_BF16)
-        hipLaunchKernelGGL(dense_nt_kernel<uint16_t>, dim3((unsigned)blocks), dim3(kDThreads), 0, st,
-                           (const uint16_t*)X, (const uint16_t*)G, Y, n, (int)p, (int)m, ldy, m_tiles, n_tiles);
-    else
-        hipLaunchKernelGGL(dense_nt_kernel<float>, dim3((unsigned)blocks), dim3(kDThreads), 0, st, (const float*)X,
-                           (const float*)G, Y, n, (int)p, (int)m, ldy, m_tiles, n_tiles);
-    HIP_TRY(hipGetLastError());
-    return RP_OK;
+    return dtype == RP_BF16 ? dispatch_dense<uint16_t>(v, X, G, Y, n, m, p, ldy, st)
+                            : dispatch_dense<float>(v, X, G, Y, n, m, p, ldy, st);
 }

@@ -5,12 +5,14 @@ Reference semantics: sklearn ``GaussianRandomProjection`` — ``components_ = rn
 ``transform(X) = X @ components_.T`` (:569-612), a plain dense GEMM (n x m) . (m x p). The
 reference scripts never call it; BASELINE lists it as the dense-contraction config.
 
-A plain GEMM is what hipBLASLt is for (MFMA, tuned per shape): this module streams X through the
-GPU in row chunks and calls torch's matmul (hipBLASLt on ROCm) in
-  * "fp32": f32 inputs, f32 MFMA (v_mfma_f32_*_f32 — exact f32 products; gfx950 has no xf32) with
-    f32 accumulation — matches numpy's sgemm within summation-order rounding (normwise 1e-5);
-  * "bf16": inputs rounded to bf16, f32 accumulation (2x HBM, 16x MFMA rate) — documented
-    reduced-precision mode, checked against an fp64 product of the bf16-rounded inputs.
+This module streams X through the GPU in row chunks and runs librp's hand-written MFMA GEMM
+(csrc/rp_dense.hip, ``rp_dense_project_device``) in
+  * "fp32": f32 inputs, f32 MFMA (v_mfma_f32_32x32x2_f32 — exact f32 products; gfx950 has no xf32)
+    with f32 accumulation — matches numpy's sgemm within summation-order rounding (normwise 1e-5);
+  * "bf16": inputs rounded to bf16, f32 accumulation (v_mfma_f32_32x32x16_bf16; 2x less HBM, 16x
+    MFMA rate) — documented reduced-precision mode, checked against an fp64 product of the
+    bf16-rounded inputs.
+f64 input (sklearn computes in X's dtype) goes to torch's f64 matmul (library GEMM).
 ``components_`` is generated bit-identically to sklearn (``srp_matrix.gaussian_random_matrix``).
 """
 from __future__ import annotations
@@ -33,11 +35,40 @@ def _torch():
     return torch
 
 
-def dense_project_device(X, C, out=None, compute: str = "fp32"):
+def dense_project_device(X, C, out=None, compute: str = "fp32", stream=None):
     """``X @ C.T`` for device tensors X (n x m) and C (p x m).
-    ``compute``: "fp32" (exact-f32 MFMA, f32 result), "fp64" (f64 MFMA, f64 result) or "bf16"
-    (bf16 inputs, f32 accumulate, f32 result)."""
+    ``compute``: "fp32" (exact-f32 MFMA, f32 result) or "bf16" (bf16 inputs, f32 accumulate, f32
+    result) run librp's hand-written MFMA GEMM (rp_dense_project_device); "fp64" (f64 MFMA, f64
+    result) goes to torch's matmul."""
     torch = _torch()
+    if compute in ("fp32", "bf16"):
+        import ctypes
+
+        from . import _native as nat
+
+        dt = torch.bfloat16 if compute == "bf16" else torch.float32
+        Xc = X.to(dt).contiguous()
+        Cc = C.to(dt).contiguous()
+        n, m = Xc.shape
+        p = Cc.shape[0]
+        if Cc.shape[1] != m:
+            raise ValueError(f"matmul: dimension mismatch {tuple(X.shape)} @ {tuple(C.shape)}.T")
+        y = out if out is not None else torch.empty(n, p, dtype=torch.float32, device=X.device)
+        if y.dtype != torch.float32 or y.shape != (n, p) or y.stride(1) != 1:
+            raise ValueError("out must be a float32 (n, p) tensor with unit column stride")
+        step = 64 if compute == "bf16" else 32
+        if m % step:  # pad the contraction (zeros add nothing)
+            padm = (m + step - 1) // step * step
+            Xc = torch.nn.functional.pad(Xc, (0, padm - m))
+            Cc = torch.nn.functional.pad(Cc, (0, padm - m))
+            m = padm
+        if stream is None:
+            stream = torch.cuda.current_stream(X.device).cuda_stream
+        nat.check(nat.load().rp_dense_project_device(
+            X.device.index or 0, ctypes.c_void_p(Xc.data_ptr()), nat.RP_BF16 if compute == "bf16" else nat.RP_F32,
+            n, m, ctypes.c_void_p(Cc.data_ptr()), p, ctypes.c_void_p(y.data_ptr()), y.stride(0),
+            ctypes.c_void_p(stream)))
+        return y
     prev = torch.backends.cuda.matmul.allow_tf32
     torch.backends.cuda.matmul.allow_tf32 = False  # never a reduced-precision f32 path
     try:
@@ -61,7 +92,7 @@ def dense_project_device(X, C, out=None, compute: str = "fp32"):
 
 
 class GaussianRandomProjection(_SkGaussianRandomProjection):
-    """sklearn ``GaussianRandomProjection`` with a GPU ``transform`` (hipBLASLt MFMA GEMM).
+    """sklearn ``GaussianRandomProjection`` with a GPU ``transform`` (librp's MFMA GEMM).
 
     Extra parameters: ``device`` (GPU ordinal), ``compute`` ("auto" = X's dtype as sklearn
     computes, or "bf16"), ``chunk_rows`` (rows of X per device GEMM; bounds device memory)."""

@@ -48,3 +48,25 @@ def test_sparse_input():
     ours = GaussianRandomProjection(n_components=256, random_state=7).fit(X)
     ref = Sk(n_components=256, random_state=7).fit(X)
     assert _rel(ours.transform(X), ref.transform(X)) < 1e-5
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("shape", [(1, 64, 1), (300, 4096, 200), (1000, 16384, 1024), (257, 192, 129)])
+def test_mfma_kernel_ragged_shapes(compute, shape):
+    """librp's MFMA GEMM on ragged tiles (rows / columns past the 128 x 128 block, m not a multiple
+    of the K step: padded) against an fp64 product of the same (bf16-rounded) operands."""
+    import torch
+    from randomprojection_amd.gaussian import dense_project_device
+
+    n, m, p = shape
+    rng = np.random.default_rng(n + m + p)
+    X = torch.as_tensor(rng.standard_normal((n, m)).astype(np.float32), device="cuda")
+    C = torch.as_tensor(rng.normal(0, 1 / 32, (p, m)).astype(np.float32), device="cuda")
+    Y = dense_project_device(X, C, compute=compute).cpu().numpy()
+    dt = torch.bfloat16 if compute == "bf16" else torch.float32
+    ref = X.to(dt).double().cpu().numpy() @ C.to(dt).double().cpu().numpy().T
+    assert Y.shape == (n, p) and Y.dtype == np.float32
+    assert _rel(Y, ref) < 1e-5  # north_star fp32 tolerance (K = 16384 f32 fma chains: ~2e-6 measured)
+    out = torch.full((n, p + 7), 7.0, device="cuda")[:, :p]  # a strided output view
+    dense_project_device(X, C, out=out, compute=compute)
+    assert np.array_equal(out.cpu().numpy(), Y)
