@@ -71,14 +71,17 @@ def _src_sha16():
 SRC_SHA16 = _src_sha16()  # keys profiles/*traffic*.json to the kernels they were measured on
 
 
-def step_kernels(plan):
-    """The kernels one rp_project_device call launches for this plan (rp_spgemm.hip)."""
+def step_kernels(plan, staged_run):
+    """The kernels one rp_project_device call runs for this plan (rp_spgemm.hip); in auto mode the
+    other branch's kernels are launched too and exit at once."""
     if plan["pipeline"] == "rowlane":
-        ks = ["lpr_main_kernel", "lpr_heavy_count_kernel", "lpr_scan_kernel", "lpr_copy_kernel",
-              "lpr_heavy_write_kernel"]
-        if plan["staged"]:
+        ks = ["lpr_main_kernel" if staged_run else "lpr_main_flat_kernel", "lpr_heavy_count_kernel",
+              "lpr_scan_kernel", "lpr_copy_kernel", "lpr_heavy_write_kernel"]
+        if staged_run:
             ks = ["lpr_count_kernel", "lpr_run_scan_kernel", "lpr_seg_scan_kernel", "lpr_partition_kernel",
                   "lpr_gather_kernel"] + ks
+        if plan["staged"] == "auto":
+            ks = ["lpr_choose_kernel"] + ks
         return ks
     ks = ["spgemm_lookback_kernel", "defer_copy_kernel"]
     return (["stage_partition_kernel", "stage_gather_kernel"] + ks) if plan["staged"] else ks
@@ -248,6 +251,7 @@ def main():
     if world > 1:
         dist.barrier()
     kernel_ms = e0.elapsed_time(e1) / args.steps
+    staged_run = P.choice(args.rows, nnz_a, ws)  # auto mode: what the device chose for these rows
     # workspace header (include/rp.h / rp_spgemm.hip Workspace): tiles taken, deferred tiles
     hdr = ws[:24].cpu().numpy().view(np.uint32)
     n_tiles_run, n_deferred = int(hdr[0]), int(hdr[4])
@@ -282,7 +286,8 @@ def main():
         except Exception:  # noqa: BLE001
             continue
         if (tj.get("rows") == args.rows and tj.get("dist") == args.dist and tj.get("src_sha16") == SRC_SHA16
-                and tj.get("pipeline") == plan["pipeline"] and bool(tj.get("staged")) == plan["staged"]):
+                and tj.get("pipeline") == plan["pipeline"] and tj.get("staged") == plan["staged"]
+                and tj.get("staged_this_call", staged_run) == staged_run):
             traffic, l2_hit = tj.get("hbm_bytes_per_launch"), tj.get("l2_hit_rate_main_kernel")
             traffic_file = os.path.relpath(f, ROOT)
             break
@@ -316,7 +321,7 @@ def main():
                          "traffic_source": f"rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per step, {traffic_file}",
                          "l2_hit_rate_r_gathers": l2_hit,
                          "pipeline": plan, "librp_src_sha16": SRC_SHA16,
-                         "step_kernels": step_kernels(plan),
+                         "step_kernels": step_kernels(plan, staged_run),
                          "traffic_GBps": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
                          "random_line_ceiling_G_per_s": RANDOM_LINE_CEILING / 1e9,
                          "gathers_G_per_s": gathers_per_s / 1e9,
@@ -325,7 +330,7 @@ def main():
             "verified": check,
             "r_setup_s": t_r,
             "r_broadcast_ms": t_bcast * 1e3,
-            "tiles": n_tiles_run, "deferred_tiles": n_deferred,
+            "tiles": n_tiles_run, "deferred_tiles": n_deferred, "staged_this_call": staged_run,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -157,11 +157,18 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
 /* The kernel pipeline rp_project_device would run for n_rows rows holding nnz_a entries with the
  * full workspace: *pipeline = RP_PIPE_TILE (one-launch tile SpGEMM with look-back) or
  * RP_PIPE_ROWLANE (row-lane kernel: short rows over a packed R), *staged = 1 if the R descriptors
- * are fetched by the staged gather, *bucket_shift its bucket width (log2 features). Any out
+ * are fetched by the staged gather, 0 if gathered directly, 2 if the device decides per call (auto
+ * mode, rp_project_choice), *bucket_shift the staged bucket width (log2 features). Any out
  * pointer may be NULL. For logging and benchmarks; results are identical on every pipeline. */
 typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1 } rp_pipeline;
 int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t* pipeline, int32_t* staged,
                     int32_t* bucket_shift);
+
+/* After a completed rp_project_device call with `workspace` on n_rows / nnz_a: *staged = 1 if that
+ * call used the staged gather, 0 if direct gathers (rp_project_plan's *staged == 2: decided on the
+ * device per call, from a sample of the input's feature ids). Synchronous (4-byte copy). */
+int rp_project_choice(const rp_projector* h, int64_t n_rows, int64_t nnz_a, const void* workspace,
+                      int32_t* staged);
 
 /* C = A @ R, all device memory, enqueued on `stream` (hipStream_t, NULL = default).
  * workspace: caller device memory of workspace_bytes (>= rp_project_workspace_bytes(h, n, -1);

@@ -22,7 +22,7 @@ EXPORTS = (
     "rp_last_error", "rp_version", "rp_device_count",
     "rp_projector_create", "rp_projector_info_get", "rp_projector_export",
     "rp_projector_create_from_device", "rp_projector_destroy", "rp_pack_r_host",
-    "rp_project_workspace_bytes", "rp_project_plan", "rp_projector_set_staging", "rp_project_device",
+    "rp_project_workspace_bytes", "rp_project_plan", "rp_project_choice", "rp_projector_set_staging", "rp_project_device",
     "rp_project_host_begin", "rp_result_fetch", "rp_result_free", "rp_project",
     "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_project_stream", "rp_host_alloc", "rp_host_free",
     "rp_dense_project_device",
@@ -108,6 +108,7 @@ def load(path: str = None):
         "rp_pack_r_host": (ctypes.c_int, [i64, i64, vp, i32, vp, i32, vp, i32, i32, P(ProjectorInfo), vp, vp, vp]),
         "rp_project_workspace_bytes": (i64, [vp, i64, i64]),
         "rp_project_plan": (ctypes.c_int, [vp, i64, i64, P(i32), P(i32), P(i32)]),
+        "rp_project_choice": (ctypes.c_int, [vp, i64, i64, vp, P(i32)]),
         "rp_projector_set_staging": (ctypes.c_int, [vp, i32, i32]),
         "rp_project_device": (ctypes.c_int, [vp, P(CsrIn), P(CsrOut), i32, vp, i64, vp, P(i64)]),
         "rp_project_host_begin": (ctypes.c_int, [vp, P(CsrIn), i32, P(vp), P(i64)]),

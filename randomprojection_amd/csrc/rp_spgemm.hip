@@ -940,11 +940,46 @@ constexpr int kRunGroup = 4096;  // tiles per group (uniform KDD2012: ~110K entr
 // [x * t8, (x + 1) * t8) in order, so neighbouring tiles are in flight on one XCD together
 __device__ __forceinline__ unsigned xcd_tile(unsigned i, unsigned t8) { return (i & 7u) * t8 + (i >> 3); }
 
+// K0 (auto staging): staged or direct gathers, decided on the device per call. 8192 entries sampled
+// evenly over the launch; the fraction of distinct features among them (an LDS hash set)
+// estimates the share of gathers that miss L2 in direct mode: uniform KDD2012-shaped columns give
+// ~100% (staging pays: configs[1] 21 ms vs 27 ms), Zipf(1.1) power-law columns ~40% (direct pays:
+// 15 ms vs 21 ms). Staged iff at least kChooseDistinctPct percent are distinct.
+constexpr int kChooseSamples = 8192, kChooseSlots = 16384, kChooseDistinctPct = 85;
+template <typename IP>
+__global__ void __launch_bounds__(1024)
+lpr_choose_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, uint32_t* __restrict__ gate) {
+    __shared__ uint32_t s_tab[kChooseSlots];
+    __shared__ uint32_t s_new;
+    for (int i = threadIdx.x; i < kChooseSlots; i += 1024) s_tab[i] = 0u;
+    if (threadIdx.x == 0) s_new = 0u;
+    __syncthreads();
+    const int64_t a0 = (int64_t)Ap[0], tot = (int64_t)Ap[n_rows] - a0;
+    const int S = (int)std::min<int64_t>(kChooseSamples, std::max<int64_t>(tot, 0));
+    for (int i = threadIdx.x; i < S; i += 1024) {
+        const uint32_t key = (uint32_t)Aj[a0 + (int64_t)i * tot / S] + 1u;
+        uint32_t h = (key * 0x9E3779B1u) >> 18;
+        while (true) {  // S < slots: always terminates
+            const uint32_t old = atomicCAS(&s_tab[h], 0u, key);
+            if (old == 0u) {
+                atomicAdd(&s_new, 1u);
+                break;
+            }
+            if (old == key) break;
+            h = (h + 1u) & (kChooseSlots - 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *gate = S > 0 && s_new * 100u >= (uint32_t)kChooseDistinctPct * (uint32_t)S ? 1u : 0u;
+}
+
 // K1: per-tile bucket histogram -> OFFT (within-tile exclusive starts)
 template <typename IP>
 __global__ void __launch_bounds__(kBlock)
 lpr_count_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, Caps caps,
-                 unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT) {
+                 unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT,
+                 const uint32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;  // the device chose direct gathers for this call
     __shared__ uint32_t s_hist[kStageMaxNB];
     __shared__ uint32_t s_wsum[kBlock / 64];
     const int tid = threadIdx.x;
@@ -981,7 +1016,8 @@ lpr_count_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int6
 constexpr int kRunPer = kRunGroup / kBlock;  // tiles per thread
 __global__ void __launch_bounds__(kBlock)
 lpr_run_scan_kernel(const uint16_t* __restrict__ OFFT, uint32_t* __restrict__ OFF2, int64_t* __restrict__ GB,
-                    unsigned n_tiles, int nb, uint32_t ostride) {
+                    unsigned n_tiles, int nb, uint32_t ostride, const uint32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
     __shared__ uint32_t s_wsum[kBlock / 64];
     const unsigned g = blockIdx.x / (unsigned)nb, b = blockIdx.x % (unsigned)nb;
     const unsigned t0 = g * kRunGroup + kRunPer * threadIdx.x;
@@ -1006,7 +1042,9 @@ lpr_run_scan_kernel(const uint16_t* __restrict__ OFFT, uint32_t* __restrict__ OF
 }
 
 // K3: segment sizes -> exclusive starts, in place (one workgroup of 1024 threads)
-__global__ void __launch_bounds__(1024) lpr_seg_scan_kernel(int64_t* __restrict__ GB, unsigned n) {
+__global__ void __launch_bounds__(1024) lpr_seg_scan_kernel(int64_t* __restrict__ GB, unsigned n,
+                                                            const uint32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
     __shared__ int64_t s[1024];
     const unsigned per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = std::min(n, lo + per);
     int64_t sum = 0;
@@ -1044,7 +1082,8 @@ __global__ void __launch_bounds__(kBlock)
 lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, Caps caps,
                      unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride,
                      const uint16_t* __restrict__ OFFT, const uint32_t* __restrict__ OFF2,
-                     const int64_t* __restrict__ GB, uint32_t* __restrict__ S) {
+                     const int64_t* __restrict__ GB, uint32_t* __restrict__ S, const uint32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
     extern __shared__ __align__(16) uint32_t s_key[];  // [cap_a]
     __shared__ uint32_t s_cur[kStageMaxNB];
     __shared__ uint16_t s_st[kStageMaxNB + 1];
@@ -1092,7 +1131,9 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
 constexpr int kGBlock = 512;  // 8 waves share one staged bitmap (64 KB at 2^19 features)
 __global__ void __launch_bounds__(kGBlock)
 lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__ BM, const int64_t* __restrict__ GB,
-                  int sb, int nb, unsigned groups, const uint32_t* __restrict__ S, uint32_t* __restrict__ D) {
+                  int sb, int nb, unsigned groups, const uint32_t* __restrict__ S, uint32_t* __restrict__ D,
+                  const uint32_t* __restrict__ gate) {
+    if (gate && *gate == 0) return;
     extern __shared__ __align__(16) uint32_t s_bm[];  // 2^sb bits
     const unsigned xcd = blockIdx.x & 7u, k = blockIdx.x >> 3;
     const unsigned b = xcd + 8u * (k / groups);
@@ -1230,6 +1271,7 @@ __device__ __forceinline__ T wave_incl_scan_t(T v, int lane) {
 
 // staged runs of the row-lane pipeline (see lpr_partition_kernel)
 struct LprStage {
+    const uint32_t* gate;  // non-NULL: staged iff *gate (lpr_choose_kernel); the direct kernel iff !*gate
     const uint16_t* offt;
     const uint32_t* off2;
     const int64_t* gb;
@@ -1239,11 +1281,495 @@ struct LprStage {
     int nb;
 };
 
+// Persistent and software-pipelined: a workgroup walks the tiles k = blockIdx.x, + gridDim.x, ...
+// (gridDim.x a multiple of 8, so all of a workgroup's tiles are in its XCD's range, xcd_tile) and
+// overlaps the memory rounds of tile k + 1 with the compute of tile k. Per tile:
+//   round 1 (only the tile index): row pointers and, staged, the tile's run table — issued before
+//            the flat pass of the previous tile;
+//   round 2 (needs round 1): staged, the S/D words of every run; direct, the feature ids (and the
+//            W gathers at the top of the tile's own iteration) — issued before the previous
+//            tile's row phase, with the first values of the flat pass;
+// so a tile's compute waits on memory only where round 2 outlasts the previous tile's row phase.
 template <typename T, typename IP, bool STAGED>
-__global__ void __launch_bounds__(kLprRows)
+__global__ void __launch_bounds__(kLprRows) __attribute__((amdgpu_waves_per_eu(4)))
 lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
                 const T* __restrict__ Ax, LprStage stg, int cap_a, unsigned n_tiles, unsigned t8, int order,
                 LprSpace sp, Workspace* ws) {
+    extern __shared__ __align__(16) unsigned char lds[];          // s_desc[cap_a] u32, 4 slots
+    __shared__ uint16_t s_rowptr[kLprRows + 1];
+    __shared__ uint64_t s_side[kLprSide];
+    __shared__ uint32_t s_sidej[kLprSide];                          // side entry's feature (staged)
+    __shared__ uint16_t s_sfk[kLprSide];                            // side entry's slot position
+    __shared__ uint8_t s_sfw[kLprSide];                             // ... in the slot of this wave
+    __shared__ T s_sfx[kLprSide];                                   // ... and its value
+    __shared__ uint64_t s_flag[4][kLprFlagWords];                  // row-start bitmap per wave
+    __shared__ uint64_t s_susp[4];                                  // rows flagged for the exact path
+    __shared__ uint16_t s_kst[4][64];
+    __shared__ uint8_t s_nz2row[4][64];
+    // side-entry count and the heavy flag, one pair per iteration parity: the next tile's pair is
+    // reset after the barrier that ends every read of it in the tile before
+    __shared__ uint32_t s_nside[2], s_wnz[4];
+    __shared__ int s_bad[2];
+    // the NEXT tile's run table (staged): element -> run, see stage_runs below
+    __shared__ uint32_t s_ksrc[STAGED ? kStageMaxNB : 1];
+    __shared__ uint64_t s_sbm[STAGED ? 64 : 1];
+    uint32_t* s_desc = reinterpret_cast<uint32_t*>(lds);
+    uint16_t* s_colbuf = reinterpret_cast<uint16_t*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)));  // 4 x slot
+    T* s_valbuf = reinterpret_cast<T*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)) +
+                                       ((8 * (size_t)sp.slot + 15) & ~size_t(15)));                // 4 x slot
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const unsigned kend = 8u * t8;
+    constexpr int kU = 12;  // round-2 words per thread held across the previous tile's row phase
+
+    // ---- round 1 of a tile: raw loads into registers (consumed one phase later)
+    struct Pre {
+        unsigned tile;
+        int nrows;
+        IP a0, an, ae0, ae1, arp0, arp1;
+        int64_t g0, gbt;
+        uint16_t st0, st1;
+        uint32_t off2;
+    };
+    auto round1 = [&](unsigned k) {
+        Pre p{};
+        p.tile = k < kend ? xcd_tile(k, t8) : n_tiles;
+        if (p.tile >= n_tiles) return p;  // uniform
+        const int64_t row0 = (int64_t)p.tile * kLprRows;
+        p.nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
+        p.a0 = Ap[row0];
+        p.an = Ap[row0 + p.nrows];
+        p.ae0 = Ap[row0 + std::min(64 * wu, p.nrows)];
+        p.ae1 = Ap[row0 + std::min(64 * wu + 64, p.nrows)];
+        p.arp0 = tid <= p.nrows ? Ap[row0 + tid] : IP(0);
+        p.arp1 = tid == 0 && p.nrows == kLprRows ? Ap[row0 + kLprRows] : IP(0);
+        if constexpr (STAGED) {
+            const size_t gb = (size_t)(p.tile / kRunGroup) * stg.nb;
+            p.g0 = stg.gb[gb];
+            if (tid < stg.nb) {
+                const size_t o = (size_t)tid * stg.ostride + p.tile;
+                p.st0 = stg.offt[o];
+                p.st1 = stg.offt[o + stg.ostride];
+                p.gbt = stg.gb[gb + tid];
+                p.off2 = stg.off2[o];
+            }
+        }
+        return p;
+    };
+    // ---- round 2 of a tile: staged S/D words (run lookup in s_ksrc / s_sbm) or direct feature ids,
+    // plus the first four value steps of the flat pass
+    uint32_t sv[kU], dv[kU];
+    constexpr int kXP = 4;  // flat-pass value steps in flight (loaded ahead of use; 8 spills: slower)
+    T xn[kXP];
+    auto run_lookup = [&](uint32_t q, uint32_t pre) {  // index of element q's word, relative to g0
+        const uint32_t k = (uint32_t)__shfl((int)pre, (int)(q >> 6), 64) +
+                           (uint32_t)__popcll(s_sbm[q >> 6] & (~0ull >> (63 - (q & 63)))) - 1u;
+        return s_ksrc[k] + q;
+    };
+    auto round2 = [&](const Pre& p, uint32_t b0, uint32_t pre) {  // words [b0, b0 + kU * 256) of the tile
+        const uint32_t ne = (uint32_t)((int64_t)p.an - (int64_t)p.a0);
+        if constexpr (STAGED) {
+            const uint32_t* __restrict__ St = stg.s + p.g0;
+            const uint32_t* __restrict__ Dt = stg.d + p.g0;
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {  // block-uniform trip count: every lane takes part in the shuffle
+                const uint32_t q0 = b0 + tid + u * kLprRows;
+                const uint32_t i = run_lookup(std::min(q0, ne - 1), pre);
+                sv[u] = q0 < ne ? St[i] : 0u;
+                dv[u] = q0 < ne ? Dt[i] : 0u;
+            }
+        } else {
+            const int32_t* __restrict__ Ajt = Aj + (int64_t)p.a0;
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const uint32_t e = b0 + tid + u * kLprRows;
+                sv[u] = e < ne ? (uint32_t)Ajt[e] : 0xffffffffu;
+            }
+        }
+    };
+    auto first_values = [&](const Pre& p) {
+        const int64_t ea = (int64_t)p.a0;
+        const uint32_t E0 = (uint32_t)((int64_t)p.ae0 - ea), E1 = (uint32_t)((int64_t)p.ae1 - ea);
+        const T* __restrict__ Axw = Ax + ea;
+        const uint32_t elast = E1 > E0 ? E1 - 1 : E0;
+#pragma unroll
+        for (int j = 0; j < kXP; ++j) {
+            const uint32_t e = E0 + 64 * j + lane;
+            const T v = Axw[std::min(e, elast)];
+            xn[j] = e < E1 ? v : T(0);
+        }
+    };
+    // staged: the run table of a tile into s_ksrc / s_sbm; returns this lane's `pre` (set bits in the
+    // start-bitmap words below word `lane`). Two block barriers.
+    auto stage_runs = [&](const Pre& p) -> uint32_t {
+        if constexpr (STAGED) {
+            const uint32_t m_st = p.st0, m_len = tid < stg.nb ? (uint32_t)p.st1 - (uint32_t)p.st0 : 0u;
+            const uint32_t m_src = (uint32_t)(p.gbt - p.g0) + p.off2;
+            if (tid < 64) s_sbm[tid] = 0ull;
+            const uint64_t nzb = __ballot(m_len > 0);
+            if (lane == 0) s_wnz[w] = (uint32_t)__popcll(nzb);
+            __syncthreads();
+            if (m_len > 0) {
+                uint32_t k = (uint32_t)__popcll(nzb & ((1ull << lane) - 1ull));
+                for (int i = 0; i < w; ++i) k += s_wnz[i];
+                s_ksrc[k] = m_src - m_st;
+                atomicOr(reinterpret_cast<unsigned long long*>(&s_sbm[m_st >> 6]), 1ull << (m_st & 63));
+            }
+            __syncthreads();
+            const uint32_t c = (uint32_t)__popcll(s_sbm[lane]);
+            return wave_scan_dpp(c) - c;
+        } else {
+            return 0u;
+        }
+    };
+    // descriptors of words [b0, b0 + kU * 256) into s_desc: the W32 word (n <= 2 entries inline);
+    // more entries -> code 3 | count << 26 | side index, the feature's W word in s_side (direct: now;
+    // staged: gathered after the descriptors, needed only after the flat pass)
+    int par = 0;  // iteration parity (s_nside / s_bad)
+    auto put_side = [&](uint32_t e, uint32_t c4, uint32_t j_or_0, uint64_t wv, bool have_w) {
+        const uint32_t k = atomicAdd(&s_nside[par], 1u);
+        if (k < (uint32_t)kLprSide) {
+            if (have_w) s_side[k] = wv;
+            s_sidej[k] = j_or_0;
+        } else {
+            s_bad[par] = 1;
+        }
+        s_desc[e] = 0xc0000000u | (c4 << 26) | k;
+    };
+    auto put_words = [&](uint32_t ne, uint32_t b0) {
+        if constexpr (STAGED) {
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (b0 + tid + u * kLprRows < ne) {
+                    if ((dv[u] >> 30) == 3) put_side(sv[u] >> 20, (dv[u] >> 26) & 15u, dv[u] & kW32J, 0ull, false);
+                    else s_desc[sv[u] >> 20] = dv[u];  // the W32 word: same bits as W's slots 0-1
+                }
+        } else {
+            uint64_t wv[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) wv[u] = sv[u] != 0xffffffffu ? R.W[sv[u]] : 0ull;
+#pragma unroll
+            for (int u = 0; u < kU; ++u)
+                if (b0 + tid + u * kLprRows < ne) {
+                    const uint64_t x = wv[u];
+                    const uint32_t n = (uint32_t)(x >> 61);
+                    if (n <= 2) s_desc[b0 + tid + u * kLprRows] = (n << 30) | (uint32_t)(x & 0x3fffffffu);
+                    else put_side(b0 + tid + u * kLprRows, std::min(n != 7 ? n : (uint32_t)R.O[x & kLow61], 15u), 0u,
+                                  x, true);
+                }
+        }
+    };
+    auto go_heavy = [&](unsigned tile) {  // one lane of the tile: the heavy path takes the whole tile
+        if (atomicOr(&sp.tflag[tile], 1u) == 0u) sp.hlist[atomicAdd(&ws->n_deferred, 1u)] = tile;
+    };
+
+    if (stg.gate && *stg.gate == 0) return;  // uniform: the device chose direct gathers for this call
+    // ---- pipeline prologue: the first tile's two rounds
+    unsigned k = blockIdx.x;
+    Pre cur = round1(k);
+    if (cur.tile >= n_tiles) return;  // uniform: no tile for this workgroup
+    if (tid == 0) {
+        s_nside[0] = 0;
+        s_bad[0] = 0;
+    }
+    uint32_t cur_pre = stage_runs(cur);  // (its barriers also publish the resets above)
+    round2(cur, 0, cur_pre);
+    first_values(cur);
+    while (true) {
+        // ---- A: this tile's descriptors into LDS
+        const unsigned tile = cur.tile;
+        const int nrows = cur.nrows;
+        const int64_t ea = (int64_t)cur.a0;
+        const int64_t ne64 = (int64_t)cur.an - ea;
+        const uint32_t ne = (uint32_t)ne64;
+        const uint32_t E0 = (uint32_t)((int64_t)cur.ae0 - ea), E1 = (uint32_t)((int64_t)cur.ae1 - ea);
+        const int64_t rp0 = (int64_t)cur.arp0, rp1 = (int64_t)cur.arp1;
+        const T* __restrict__ Axw = Ax + ea;
+        T xv[kXP];
+#pragma unroll
+        for (int j = 0; j < kXP; ++j) xv[j] = xn[j];
+        const bool too_many = ne64 > cap_a;  // uniform
+        __syncthreads();  // previous tile done with s_desc / slots / side table / its flags
+        STAMP(0);
+        if (tid == 0) {  // the next tile's pair (its last readers were the tile before this one)
+            s_nside[par ^ 1] = 0;
+            s_bad[par ^ 1] = 0;
+        }
+        if (!too_many) {
+            put_words(ne, 0);
+            // the rest of a large tile, synchronously (rare); s_ksrc / s_sbm still hold its runs
+            for (uint32_t b0 = kU * kLprRows; b0 < ne; b0 += kU * kLprRows) {
+                round2(cur, b0, cur_pre);
+                put_words(ne, b0);
+            }
+        }
+        if (tid <= nrows) s_rowptr[tid] = (uint16_t)(rp0 - ea);
+        if (tid == 0 && nrows == kLprRows) s_rowptr[kLprRows] = (uint16_t)(rp1 - ea);
+        STAMP(1);
+        // ---- the next tile's round 1, in flight during this tile's flat pass
+        k += gridDim.x;
+        const Pre nxt = round1(k);
+        __syncthreads();
+        STAMP(2);
+        const bool skip = too_many || s_bad[par] != 0;  // uniform: too many entries or the side table is full
+        if (skip && tid == 0) go_heavy(tile);
+        // staged: the W words of the side entries are gathered now and only needed after the flat
+        // pass (their counts came with the staged words), so this latency hides behind the pass
+        const uint32_t nside = skip ? 0u : s_nside[par];
+        uint64_t sidew = 0;
+        if (STAGED && (uint32_t)tid < nside) sidew = R.W[s_sidej[tid]];
+        // ---- step B: one wave per 64 rows, one flat pass over the wave's entries
+        const int r = tid;  // this lane's row (for per-row work)
+        const bool valid = r < nrows;
+        const uint32_t rs = valid ? s_rowptr[r] : 0u, re = valid ? s_rowptr[r + 1] : 0u;
+        const uint32_t nsteps = skip ? 0u : (E1 - E0 + 63) >> 6;
+        for (uint32_t q = lane; q < nsteps; q += 64) s_flag[w][q] = 0ull;
+        if (lane == 0) s_susp[w] = 0ull;
+        __builtin_amdgcn_wave_barrier();
+        const bool nonempty = !skip && re > rs;
+        const uint64_t ne_mask = __ballot(nonempty);
+        if (nonempty) {
+            const uint32_t b = rs - E0;
+            atomicOr(reinterpret_cast<unsigned long long*>(&s_flag[w][b >> 6]), 1ull << (b & 63));
+            s_nz2row[w][__builtin_popcountll(ne_mask & ((1ull << lane) - 1))] = (uint8_t)lane;
+        }
+        __builtin_amdgcn_wave_barrier();
+        // the wave's slot is built in LDS (columns cb, values vb, first-touch order) and stored to
+        // HBM with coalesced stores at the end
+        uint16_t* cb = s_colbuf + (size_t)w * sp.slot;
+        T* vb = s_valbuf + (size_t)w * sp.slot;
+        uint32_t carry_r = 0, carry_k = 0;
+        const T nmag = -mag;
+        auto ldx = [&](uint32_t j) {
+            const uint32_t e = E0 + 64 * j + lane;
+            const uint32_t elast = E1 > E0 ? E1 - 1 : E0;
+            const T v = Axw[std::min(e, elast)];
+            return e < E1 ? v : T(0);
+        };
+        auto step = [&](uint32_t j, T x) {
+            const uint32_t e = E0 + 64 * j + lane;
+            const bool ve = e < E1;
+            const uint64_t fw = s_flag[w][j];
+            const uint32_t nr = carry_r + (uint32_t)__builtin_popcountll(fw & ((2ull << lane) - 1)) - 1u;
+            const uint32_t row = s_nz2row[w][nr & 63];
+            const uint32_t d = ve ? s_desc[e] : 0u;
+            const uint32_t n = d >> 30;
+            const uint32_t np = n < 3 ? n : (d >> 26) & 15u;  // n == 3: a side entry (count in the word)
+            const bool nzx = tmul<T>(x, mag) != T(0);  // all products of an entry share |x * mag|
+            const uint32_t kc = nzx ? np : 0u;
+            const uint32_t kinc = wave_scan_dpp(kc);
+            const uint32_t K = carry_k + kinc - kc;
+            if (ve && ((fw >> lane) & 1ull)) s_kst[w][row] = (uint16_t)K;  // the row's first entry
+            const uint32_t sl0 = d & 0x7fffu, sl1 = (d >> 15) & 0x7fffu;
+            if (n < 3 && kc >= 1 && K < sp.slot) {
+                cb[K] = (uint16_t)(sl0 & 0x3fffu);
+                vb[K] = tadd<T>(T(0), tmul<T>(x, (sl0 & 0x4000u) ? nmag : mag));
+            }
+            if (n < 3 && kc >= 2 && K + 1 < sp.slot) {
+                cb[K + 1] = (uint16_t)(sl1 & 0x3fffu);
+                vb[K + 1] = tadd<T>(T(0), tmul<T>(x, (sl1 & 0x4000u) ? nmag : mag));
+            }
+            // side entries keep a gap [K, K + np) in the slot, filled after the pass (their W words
+            // may still be in flight); a zero product is not in the slot: its row takes the exact path
+            if (n == 3) {
+                const uint32_t kk = d & kW32J;
+                s_sfk[kk] = kc ? (uint16_t)K : (uint16_t)0xffffu;
+                s_sfw[kk] = (uint8_t)w;
+                s_sfx[kk] = x;
+                if (np == 15) s_bad[par] = 1;  // 15 or more entries: the count is not exact -> heavy tile
+            }
+            if (ve && np > 0 && !nzx) atomicOr(reinterpret_cast<unsigned long long*>(&s_susp[w]), 1ull << row);
+            carry_k += __builtin_amdgcn_readlane(kinc, 63);
+            carry_r += (uint32_t)__builtin_popcountll(fw);
+        };
+        // values straight from HBM in entry order (coalesced), kXP steps in flight ahead of use
+        for (uint32_t j = 0; j < nsteps; j += kXP) {
+            T c[kXP];
+#pragma unroll
+            for (int u = 0; u < kXP; ++u) {
+                c[u] = xv[u];
+                xv[u] = ldx(j + kXP + u);
+            }
+#pragma unroll
+            for (int u = 0; u < kXP; ++u)
+                if (j + u < nsteps) step(j + u, c[u]);
+        }
+        bool overflow = carry_k > sp.slot;
+        __syncthreads();
+        // side fill: every side entry's products into its gap, in R's storage order
+        if ((uint32_t)tid < nside) {
+            const uint64_t sw = STAGED ? sidew : s_side[tid];
+            if (STAGED) s_side[tid] = sw;
+            const uint32_t k0 = s_sfk[tid];
+            if (k0 != 0xffffu) {
+                uint16_t* cbw = s_colbuf + (size_t)s_sfw[tid] * sp.slot;
+                T* vbw = s_valbuf + (size_t)s_sfw[tid] * sp.slot;
+                const T x = s_sfx[tid];
+                const bool rec = (sw >> 61) == 7;
+                const uint32_t np = rec ? R.O[sw & kLow61] : (uint32_t)(sw >> 61);
+                for (uint32_t t = 0; t < np && k0 + t < sp.slot; ++t) {
+                    uint32_t sl;
+                    if (rec) {
+                        const uint32_t e = R.O[(sw & kLow61) + 1 + t];
+                        sl = ((e & 0x8000u) >> 1) | (e & 0x3fffu);
+                    } else {
+                        sl = (uint32_t)(sw >> (15 * t)) & 0x7fffu;
+                    }
+                    cbw[k0 + t] = (uint16_t)(sl & 0x3fffu);
+                    vbw[k0 + t] = tadd<T>(T(0), tmul<T>(x, (sl & 0x4000u) ? -mag : mag));
+                }
+            }
+        }
+        // ---- the next tile's round 2, in flight during this tile's row phase
+        const uint32_t npre = nxt.tile < n_tiles ? stage_runs(nxt) : 0u;  // two barriers (staged)
+        __syncthreads();
+        const bool bad2 = s_bad[par] != 0;  // uniform: a side entry with 15 or more products
+        if (nxt.tile < n_tiles) {
+            round2(nxt, 0, npre);
+            first_values(nxt);
+        }
+        if (!skip && bad2 && tid == 0) go_heavy(tile);
+        STAMP(3);
+        if (!skip && !bad2) {
+            // ---- per row: kept count and a Bloom check of its columns (3 x 64-bit filters in
+            // registers): a column whose 3 bits are all set already flags the row for the exact
+            // path (every real repeat does; false alarms ~ (i/64)^3 for the i-th product)
+            const uint32_t kst = nonempty ? s_kst[w][lane] : 0u;
+            const uint64_t after = ne_mask & ~((2ull << lane) - 1);  // the next non-empty row ends this one
+            const int nx = after ? __builtin_ctzll(after) : 64;
+            const uint32_t kst_next = __shfl(kst, nx & 63, 64);
+            const uint32_t kend_r = nx < 64 ? kst_next : carry_k;
+            uint32_t kept = nonempty ? kend_r - kst : 0u;
+            bool hit = false;
+            if (!overflow) {
+                uint64_t b0 = 0, b1 = 0, b2 = 0;
+                for (uint32_t q = kst; q < kend_r; ++q) {
+                    const uint32_t col = cb[q];
+                    const uint64_t m0 = 1ull << (col & 63), m1 = 1ull << ((col >> 6) & 63), m2 = 1ull << lpr_h2(col);
+                    hit |= (b0 & m0) && (b1 & m1) && (b2 & m2);
+                    b0 |= m0;
+                    b1 |= m1;
+                    b2 |= m2;
+                }
+            }
+            uint64_t todo = s_susp[w] | __ballot(hit);  // lane == row within the wave
+            __builtin_amdgcn_wave_barrier();  // the row-start bitmap is dead from here: the scratch reuses it
+            constexpr int kScr = (int)((kLprFlagWords * 8 - 16) / (2 + sizeof(T)));
+            uint16_t* scol = reinterpret_cast<uint16_t*>(&s_flag[w][0]);
+            T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(&s_flag[w][0]) + ((2 * kScr + 15) & ~15));
+            if (__ballot(overflow)) todo = 0;
+            // exact path, one flagged row at a time, the whole wave on it: its products in sequence
+            // order into the scratch, then every product checks for an earlier one of its column
+            // (first touch); a leader sums its group in order; kept leaders land in the row's slot
+            // range in that order
+            while (todo) {
+                const int R0 = __builtin_ctzll(todo);
+                todo &= todo - 1;
+                const uint32_t a0 = __shfl(rs, R0, 64), a1 = __shfl(re, R0, 64), kR = __shfl(kst, R0, 64);
+                uint32_t nprod = 0;
+                for (uint32_t e0 = a0; e0 < a1; e0 += 64) {
+                    const uint32_t e = e0 + lane;
+                    const bool in = e < a1;
+                    const uint32_t d = in ? s_desc[e] : 0u;
+                    const T x = in ? Axw[e] : T(0);
+                    const uint32_t np = in ? ((d >> 30) < 3 ? (d >> 30) : (d >> 26) & 15u) : 0u;
+                    const uint32_t inc = wave_scan_dpp(np);
+                    const uint32_t q0 = nprod + inc - np;
+                    for (uint32_t t = 0; t < np; ++t)
+                        if (q0 + t < (uint32_t)kScr) {
+                            const uint32_t sl = lpr_slot(d, t, s_side, R.O);
+                            scol[q0 + t] = (uint16_t)(sl & 0x3fffu);
+                            sval[q0 + t] = tmul<T>(x, (sl & 0x4000u) ? -mag : mag);
+                        }
+                    nprod += __builtin_amdgcn_readlane(inc, 63);
+                }
+                if (nprod > (uint32_t)kScr) {
+                    overflow = true;
+                    break;
+                }
+                __builtin_amdgcn_wave_barrier();
+                uint32_t nk = 0;
+                for (uint32_t q0 = 0; q0 < nprod; q0 += 64) {
+                    const uint32_t q = q0 + lane;
+                    bool lead = q < nprod;
+                    T sum = T(0);
+                    if (lead) {
+                        const uint16_t cq = scol[q];
+                        for (uint32_t b = 0; b < q && lead; ++b) lead = scol[b] != cq;
+                        if (lead) {
+                            sum = tadd<T>(T(0), sval[q]);
+                            for (uint32_t b = q + 1; b < nprod; ++b)
+                                if (scol[b] == cq) sum = tadd<T>(sum, sval[b]);
+                        }
+                    }
+                    const bool keep = lead && sum != T(0);
+                    const uint32_t ki = wave_scan_dpp(keep ? 1u : 0u);
+                    if (keep) {
+                        if (kR + nk + ki - 1 >= sp.slot) overflow = true;
+                        else {
+                            cb[kR + nk + ki - 1] = scol[q];
+                            vb[kR + nk + ki - 1] = sum;
+                        }
+                    }
+                    nk += __builtin_amdgcn_readlane(ki, 63);
+                }
+                if (lane == R0) kept = nk;
+                __builtin_amdgcn_wave_barrier();
+            }
+            // a row that gained entries in the exact path (its side entries were not in the slot)
+            // must still end before the next row's range
+            if (kst + kept > kend_r && nonempty) overflow = true;
+            if (__ballot(overflow)) {  // this wave cannot finish on the fast path: the whole tile goes heavy
+                if (lane == 0) go_heavy(tile);
+            } else {
+                if (order == RP_ORDER_SORTED && kept > 1) {  // ascending columns inside the row's slot range
+                    for (uint32_t a = kst + 1; a < kst + kept; ++a) {
+                        const uint16_t kc = cb[a];
+                        const T kv = vb[a];
+                        uint32_t b = a;
+                        while (b > kst && cb[b - 1] > kc) {
+                            cb[b] = cb[b - 1];
+                            vb[b] = vb[b - 1];
+                            --b;
+                        }
+                        cb[b] = kc;
+                        vb[b] = kv;
+                    }
+                }
+                if (valid) sp.rowmeta[(size_t)tile * kLprRows + r] = (kst << 16) | kept;
+                const uint32_t wtot = __builtin_amdgcn_readlane(wave_scan_dpp(valid ? kept : 0u), 63);
+                if (lane == 0) sp.cnt[(size_t)tile * 4 + w] = wtot;
+                // the slot to HBM, coalesced (rows may end before their kept range when the exact
+                // path dropped entries: the whole used range goes, the copy kernel reads each row's
+                // own part)
+                __builtin_amdgcn_wave_barrier();
+                uint16_t* __restrict__ oc = sp.cols + ((size_t)tile * 4 + w) * sp.slot;
+                T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + ((size_t)tile * 4 + w) * sp.slot;
+                for (uint32_t q = lane; q < carry_k; q += 64) {
+                    oc[q] = cb[q];
+                    ov[q] = vb[q];
+                }
+            }
+        }
+        STAMP(4);
+        STAMP(5);
+        STAMP(6);
+        if (nxt.tile >= n_tiles) break;  // uniform
+        cur = nxt;
+        cur_pre = npre;
+        par ^= 1;
+    }
+}
+
+// One workgroup per tile, no persistence (direct gathers: the two dependent rounds, feature ids
+// then W words, are cheaper to hide with more resident tiles than with cross-tile pipelining;
+// measured: power-law direct main kernel 12.4 ms here vs 15.3 ms persistent)
+template <typename T, typename IP, bool STAGED>
+__global__ void __launch_bounds__(kLprRows)
+lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                const T* __restrict__ Ax, LprStage stg, int cap_a, unsigned n_tiles, unsigned t8, int order,
+                LprSpace sp, Workspace* ws) {
+    if (!STAGED && stg.gate && *stg.gate != 0) return;  // uniform: the device chose the staged gather
     extern __shared__ __align__(16) unsigned char lds[];          // s_desc[cap_a] u32
     __shared__ uint16_t s_rowptr[kLprRows + 1];
     __shared__ uint64_t s_side[kLprSide];
@@ -1989,7 +2515,9 @@ struct Plan {
     bool lpr = false;
     uint32_t lpr_slot = 0;
     int64_t lpr_chunk = 0;    // rows per launch sequence (a multiple of kLprRows; n_rows if one)
-    size_t carry = 0;         // two u64 running-total slots (chunk k reads k & 1, writes the other)
+    size_t carry = 0;         // two u64 running-total slots (chunk k reads k & 1, writes the other),
+                              // then the u32 staging gate (lpr_choose_kernel) at carry + 16
+    bool gated = false;       // staging decided on the device per call (auto mode)
     size_t zero = 0;          // bytes zeroed once per call (header + states [+ carry])
     int64_t scan_blocks = 0;
     size_t lcnt = 0, loff = 0, lhl = 0, ltf = 0, lrow = 0, lcols = 0, lvals = 0;
@@ -2072,6 +2600,7 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
             while (h->stage_sb <= 0 && nbk(sb) > kStageMaxNB && sb < 20) ++sb;
             if (sb >= 1 && sb <= 20 && nbk(sb) <= kStageMaxNB) {
                 pl.staged = true;
+                pl.gated = h->stage_mode == -1;
                 pl.sb = sb;
                 pl.nb = std::max(nbk(sb), 1);
                 pl.ostride = (uint32_t)((pl.n_tiles + 31) & ~int64_t(31));
@@ -2206,7 +2735,9 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
     const IP* Ap = (const IP*)a->indptr;
     const T* Ax = (const T*)a->data;
     const unsigned t8 = (n_tiles + 7) / 8;
+    uint32_t* gate = pl.gated ? reinterpret_cast<uint32_t*>(base + pl.carry + 16) : nullptr;
     LprStage stg{};
+    stg.gate = gate;
     if (pl.staged) {
         uint16_t* OFFT = reinterpret_cast<uint16_t*>(base + pl.offt);
         uint32_t* OFF2 = reinterpret_cast<uint32_t*>(base + pl.off2);
@@ -2214,41 +2745,53 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
         uint32_t* Sw = reinterpret_cast<uint32_t*>(base + pl.s);
         uint32_t* Dw = reinterpret_cast<uint32_t*>(base + pl.d);
         hipLaunchKernelGGL((lpr_count_kernel<IP>), dim3(8 * t8), dim3(kBlock), 0, st, Ap, a->indices, a->n_rows,
-                           pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, OFFT);
+                           pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, OFFT, gate);
         HIP_TRY(hipGetLastError());
         const unsigned nseg = pl.groups * (unsigned)pl.nb;
         hipLaunchKernelGGL(lpr_run_scan_kernel, dim3(nseg), dim3(kBlock), 0, st, (const uint16_t*)OFFT, OFF2, GB,
-                           n_tiles, pl.nb, pl.ostride);
+                           n_tiles, pl.nb, pl.ostride, gate);
         HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(lpr_seg_scan_kernel, dim3(1), dim3(1024), 0, st, GB, nseg);
+        hipLaunchKernelGGL(lpr_seg_scan_kernel, dim3(1), dim3(1024), 0, st, GB, nseg, gate);
         HIP_TRY(hipGetLastError());
         const size_t plds = 4 * (size_t)pl.caps.cap_a;
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_partition_kernel<IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)plds));
         hipLaunchKernelGGL((lpr_partition_kernel<IP>), dim3(8 * t8), dim3(kBlock), plds, st, Ap, a->indices,
                            a->n_rows, pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, (const uint16_t*)OFFT,
-                           (const uint32_t*)OFF2, (const int64_t*)GB, Sw);
+                           (const uint32_t*)OFF2, (const int64_t*)GB, Sw, gate);
         HIP_TRY(hipGetLastError());
         const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * pl.groups;
         const size_t glds = (size_t)4 << (pl.sb - 5);
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_gather_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds));
         hipLaunchKernelGGL(lpr_gather_kernel, dim3(grid), dim3(kGBlock), glds, st, (const uint32_t*)h->W32.p,
                            (const uint32_t*)h->BM.p, (const int64_t*)GB, pl.sb, pl.nb, pl.groups,
-                           (const uint32_t*)Sw, Dw);
+                           (const uint32_t*)Sw, Dw, gate);
         HIP_TRY(hipGetLastError());
-        stg = LprStage{OFFT, OFF2, GB, Sw, Dw, pl.ostride, pl.nb};
+        stg = LprStage{gate, OFFT, OFF2, GB, Sw, Dw, pl.ostride, pl.nb};
     }
     const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot, pl.staged);
+    // persistent grid: as many workgroups as can be resident (a multiple of 8: each stays in its
+    // XCD's tile range), never more than the tiles
+    auto grid_for = [&](const void* fn) -> unsigned {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kLprRows, lds) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 8)
+            cus = 256;
+        const unsigned want = ((unsigned)(per_cu * cus) + 7u) & ~7u;
+        return std::min(want, 8u * t8);
+    };
     if (pl.staged) {
-        HIP_TRY(hipFuncSetAttribute((const void*)lpr_main_kernel<T, IP, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds));
-        hipLaunchKernelGGL((lpr_main_kernel<T, IP, true>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag, a->n_rows,
-                           Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
-    } else {
-        HIP_TRY(hipFuncSetAttribute((const void*)lpr_main_kernel<T, IP, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)lds));
-        hipLaunchKernelGGL((lpr_main_kernel<T, IP, false>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag, a->n_rows,
-                           Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
+        const void* fn = (const void*)lpr_main_kernel<T, IP, true>;
+        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((lpr_main_kernel<T, IP, true>), dim3(grid_for(fn)), dim3(kLprRows), lds, st, R, mag,
+                           a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
+    }
+    if (!pl.staged || pl.gated) {  // direct gathers (gated: runs iff the device chose them)
+        const void* fn = (const void*)lpr_main_flat_kernel<T, IP, false>;
+        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((lpr_main_flat_kernel<T, IP, false>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag,
+                           a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
     }
     HIP_TRY(hipGetLastError());
     const size_t hl = heavy_lds_bytes(h->p, sizeof(T));
@@ -2283,6 +2826,11 @@ template <typename T, typename IP, typename OP, typename OI>
 int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
                Workspace* ws, const Plan& pl, hipStream_t st) {
     const int64_t n = a->n_rows, step = std::max<int64_t>(pl.lpr_chunk, 1);
+    if (pl.gated && n > 0) {  // staged or direct for this call, decided on the device (K0)
+        hipLaunchKernelGGL((lpr_choose_kernel<IP>), dim3(1), dim3(1024), 0, st, (const IP*)a->indptr, a->indices, n,
+                           reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + pl.carry + 16));
+        HIP_TRY(hipGetLastError());
+    }
     int64_t k = 0;
     for (int64_t r0 = 0; r0 < n; r0 += step, ++k) {
         rp_csr_in sa = *a;
@@ -2790,8 +3338,24 @@ int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_
     if (!h || n_rows < 0) return fail(RP_ERR_INVALID, "NULL projector or n_rows < 0");
     const Plan pl = make_plan(h, n_rows, nnz_a);
     if (pipeline) *pipeline = pl.lpr ? RP_PIPE_ROWLANE : RP_PIPE_TILE;
-    if (staged) *staged = pl.staged ? 1 : 0;
+    if (staged) *staged = pl.gated ? 2 : pl.staged ? 1 : 0;
     if (bucket_shift) *bucket_shift = pl.staged ? pl.sb : 0;
+    return RP_OK;
+}
+
+int rp_project_choice(const rp_projector* h, int64_t n_rows, int64_t nnz_a, const void* workspace,
+                      int32_t* staged) {
+    if (!h || !staged) return fail(RP_ERR_INVALID, "NULL argument");
+    const Plan pl = make_plan(h, n_rows, nnz_a);
+    if (!pl.gated) {
+        *staged = pl.staged ? 1 : 0;
+        return RP_OK;
+    }
+    if (!workspace) return fail(RP_ERR_INVALID, "the choice lives in the caller's workspace");
+    uint32_t g = 0;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipMemcpy(&g, reinterpret_cast<const char*>(workspace) + pl.carry + 16, 4, hipMemcpyDeviceToHost));
+    *staged = g ? 1 : 0;
     return RP_OK;
 }
 

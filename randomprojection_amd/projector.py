@@ -309,12 +309,21 @@ class Projector:
 
     def plan(self, n_rows: int, nnz_a: int = -1) -> dict:
         """The kernel pipeline ``project_device`` runs for this shape with a full workspace
-        (rp_project_plan): {"pipeline": "tile"|"rowlane", "staged": bool, "bucket_shift": int}."""
+        (rp_project_plan): {"pipeline": "tile"|"rowlane", "staged": bool | "auto" (decided on the device
+        per call, see ``choice``), "bucket_shift": int}."""
         pipe, st, sb = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         nat.check(self._lib.rp_project_plan(self._h, int(n_rows), int(nnz_a), ctypes.byref(pipe), ctypes.byref(st),
                                             ctypes.byref(sb)))
-        return {"pipeline": "rowlane" if pipe.value == 1 else "tile", "staged": bool(st.value),
-                "bucket_shift": int(sb.value)}
+        return {"pipeline": "rowlane" if pipe.value == 1 else "tile",
+                "staged": "auto" if st.value == 2 else bool(st.value), "bucket_shift": int(sb.value)}
+
+    def choice(self, n_rows: int, nnz_a: int, workspace) -> bool:
+        """After a completed ``project_device`` call with ``workspace`` (torch uint8 tensor): whether
+        it ran the staged gather (auto mode decides on the device per call)."""
+        st = ctypes.c_int32()
+        ptr = int(workspace.data_ptr()) if hasattr(workspace, "data_ptr") else int(workspace)
+        nat.check(self._lib.rp_project_choice(self._h, int(n_rows), int(nnz_a), ctypes.c_void_p(ptr), ctypes.byref(st)))
+        return bool(st.value)
 
     def set_staging(self, mode: str = "auto", bucket_shift: int = 0):
         """Staged gather: "auto", "off" or "on" (identical results)."""

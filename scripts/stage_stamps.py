@@ -57,7 +57,7 @@ def main():
     t0 = st[:, 0].min()
     names = ["gather-or-staged-read(1a)", "scan(1b)", "products(1c)", "accumulate(2)", "scan+lookback(3a)", "write(3b)"]
     if args.lpr:
-        names = ["stepA-loads+lds", "barrier1", "flatpass", "rows+exact+meta", "-", "-"]
+        names = ["descs(wait round2)", "barrier+round1-issue", "flatpass+side+next-runs", "rows+exact+slot-store", "-", "-"]
     res = {"tiles": int(n_tiles), "heavy_tiles": int((st[:, 7] > 0).sum())}
     ok = st[:, 6] > 0
     for k, nm in enumerate(names):

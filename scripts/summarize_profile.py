@@ -26,9 +26,10 @@ import shutil
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel", "stage_partition_kernel", "stage_gather_kernel",
                 "lpr_count_kernel", "lpr_run_scan_kernel", "lpr_seg_scan_kernel", "lpr_partition_kernel",
-                "lpr_gather_kernel", "lpr_main_kernel", "lpr_heavy_count_kernel", "lpr_scan_kernel",
+                "lpr_gather_kernel", "lpr_main_kernel", "lpr_main_flat_kernel", "lpr_choose_kernel",
+                "lpr_heavy_count_kernel", "lpr_scan_kernel",
                 "lpr_copy_kernel", "lpr_heavy_write_kernel")
-MAIN_KERNELS = ("lpr_main_kernel", "spgemm_lookback_kernel")
+MAIN_KERNELS = ("lpr_main_kernel", "lpr_main_flat_kernel", "spgemm_lookback_kernel")
 
 
 def short(name):
@@ -105,11 +106,14 @@ def main():
     summary["step"] = derive(dict(step_c), step_ms)
     json.dump(summary, open(os.path.join(prof, f"{args.tag}_summary.json"), "w"), indent=1)
     plan = roof.get("pipeline", {})
-    summary.update(pipeline=plan.get("pipeline"), staged=plan.get("staged"), src_sha16=roof.get("librp_src_sha16"))
-    main_k = next((k for k in MAIN_KERNELS if k in summary["kernels"]), None)
+    summary.update(pipeline=plan.get("pipeline"), staged=plan.get("staged"), src_sha16=roof.get("librp_src_sha16"),
+                   staged_this_call=bench.get("staged_this_call"))
+    mains = [k for k in MAIN_KERNELS if summary["kernels"].get(k, {}).get("avg_ms")]
+    main_k = max(mains, key=lambda k: summary["kernels"][k]["avg_ms"]) if mains else None  # the one that ran
     if "hbm_bytes" in summary["step"]:
         tj = {"tag": args.tag, "rows": args.rows, "dist": args.dist,
               "pipeline": plan.get("pipeline"), "staged": plan.get("staged"), "src_sha16": roof.get("librp_src_sha16"),
+              "staged_this_call": bench.get("staged_this_call"),
               "hbm_bytes_per_launch": summary["step"]["hbm_bytes"],
               "main_kernel": main_k,
               "l2_hit_rate_main_kernel": summary["kernels"].get(main_k, {}).get("l2_hit_rate"),

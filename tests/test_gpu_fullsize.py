@@ -54,6 +54,7 @@ def project(P, Ap, Aj, Ax, order="scipy", slack=1.02):
         Cx = torch.empty(cap, dtype=torch.float32, device=dev)
         try:
             nnz = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=order, workspace=ws, nnz_a=nnz_a)
+            project.staged = P.choice(n, nnz_a, ws)  # what the device chose (auto mode)
             return Cp, Cj, Cx, nnz
         except nat.RPError as e:
             if e.code != nat.RP_ERR_CAPACITY:
@@ -81,7 +82,10 @@ def test_configs1_full_size(kdd, dist, monkeypatch):
             # the whole output against the other pipeline (the tile kernel with direct gathers):
             # every byte equal, so a rare tile shape mishandled by either one cannot hide between
             # the sampled rows
-            assert P.plan(KDD_ROWS, Aj.numel()) == {"pipeline": "rowlane", "staged": True, "bucket_shift": 19}
+            assert P.plan(KDD_ROWS, Aj.numel()) == {"pipeline": "rowlane", "staged": "auto", "bucket_shift": 19}
+            # the device's choice: staged gathers for uniform columns (each gather a fresh line),
+            # direct for power-law ones (hot features stay in L2)
+            assert project.staged == (dist == "uniform")
             monkeypatch.setenv("RP_PIPE", "tile")
             P.set_staging("off")
             Tp, Tj, Tx, tn = project(P, Ap, Aj, Ax, order=order)

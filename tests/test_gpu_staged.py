@@ -251,3 +251,38 @@ def test_rowlane_staged_tile_past_one_round(R2m_p1k, monkeypatch):
     assert_same_csr(P.matmul(A), *want)
     assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
     P.close()
+
+
+@pytest.mark.parametrize("dist", ["uniform", "powerlaw"])
+def test_auto_staging_choice_on_device(dist):
+    """Auto mode on a launch large enough to stage (>= 4M entries, R's W table >= 64 MB): the device
+    samples the feature ids and picks the staged gather for uniform columns, direct gathers for
+    power-law ones; either way the whole output equals the forced pipelines' and the oracle's."""
+    import torch
+    from randomprojection_amd import synth
+
+    m, p, n = 10_000_000, 256, 420_000
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    Ap, Aj, Ax = synth.kdd_rows_device(n, m, seed=33, dist=dist)
+    nnz_a = int(Aj.numel())
+    outs = {}
+    for mode in ("auto", "on", "off"):
+        P = Projector(R)
+        P.set_staging(mode)
+        plan = P.plan(n, nnz_a)
+        assert plan["pipeline"] == "rowlane" and plan["staged"] == {"auto": "auto", "on": True, "off": False}[mode]
+        ws = torch.empty(P.workspace_bytes(n, nnz_a), dtype=torch.uint8, device="cuda")
+        cap = int(3 * nnz_a * P.nnz / P.m) + 65536  # hot power-law features may carry more R entries
+        Cp = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+        Cj = torch.empty(cap, dtype=torch.int32, device="cuda")
+        Cx = torch.empty(cap, dtype=torch.float32, device="cuda")
+        k = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, workspace=ws, nnz_a=nnz_a)
+        if mode == "auto":
+            assert P.choice(n, nnz_a, ws) == (dist == "uniform")
+        outs[mode] = (Cp.cpu().numpy(), Cj[:k].cpu().numpy(), Cx[:k].cpu().numpy())
+        P.close()
+    A = sp.csr_matrix((Ax.cpu().numpy(), Aj.cpu().numpy(), Ap.cpu().numpy()), shape=(n, m))
+    want = oracle_product(A, R)
+    for mode, (cp, cj, cx) in outs.items():
+        assert np.array_equal(cp, want[0]) and np.array_equal(cj, want[1]), mode
+        assert np.array_equal(cx.view(np.uint32), want[2].view(np.uint32)), mode
