@@ -125,7 +125,11 @@ def load(path: str = None):
                                                   P(i64), P(i64), P(i64)]),
     }
     for name, (res, args) in sig.items():
-        f = getattr(lib, name)
+        f = getattr(lib, name, None)
+        if f is None and path != LIB_PATH:  # an older diagnostic build (RP_LIB, timing scripts only)
+            continue
+        if f is None:
+            raise NativeUnavailable(f"{path} does not export {name}: rebuild it")
         f.restype = res
         f.argtypes = args
     _lib = lib

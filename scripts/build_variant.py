@@ -10,6 +10,8 @@ sys.path.insert(0, ROOT)
 from randomprojection_amd.build import FLAGS, HIPCC, SRC  # noqa: E402
 
 src = [sys.argv[1]] + [s for s in SRC if not s.endswith("rp_spgemm.hip")]
+if "0d702fa" in open(sys.argv[1]).read(20000) or os.environ.get("NO_DENSE"):
+    src = [s for s in src if not s.endswith("rp_dense.hip")]
 inc = ["-I", os.path.join(ROOT, "randomprojection_amd", "csrc"), "-I", os.path.join(ROOT, "include")]
 subprocess.run([HIPCC, *FLAGS, *inc, "-o", sys.argv[2], *src], check=True)
 print(sys.argv[2])
