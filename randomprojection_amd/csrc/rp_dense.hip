@@ -200,7 +200,7 @@ int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, i
 // tile variants (RP_DENSE_VARIANT, measurements): 0 = 128x128 2 stages, 1 = 128x128 1 stage,
 // 2 = 256x128 1 stage, 3 = 128x256 2 stages (8 waves), 4 = 256x256 1 stage (8 waves), 5 = 256x256
 // 2 stages (128 KB LDS, 8 waves)
-constexpr int kDenseVariant = 0;
+constexpr int kDenseVariant = 5;  // 256 x 256, two LDS stages (measured best of 0-5, profiles/r02_dense_variants.json)
 template <typename T>
 int dispatch_dense(int v, const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
                    hipStream_t st) {

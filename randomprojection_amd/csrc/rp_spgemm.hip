@@ -7,18 +7,19 @@
 // (jj, kk) storage order, each multiply rounded, then added into sums[k] (starting at +0); output
 // entries = distinct touched k with sums[k] != 0, in reverse first-touch order (or ascending).
 //
-// Design: one launch, one workgroup per tile of up to 256 rows, tiles taken in
-// dispatch order from an atomic counter, and a single-pass decoupled look-back over tile nnz so
-// the output is written exactly once at its final CSR position:
-//   stage 1  (flat over the tile's A entries, coalesced): gather each feature's R row descriptor
-//            (packed: one u16 word per feature, L2/MALL resident) and scan product counts in LDS;
-//            write every product x*b (rounded once) into an LDS product array, grouped by row.
-//   stage 2  (one lane per row): walk the row's products in order, accumulating into a list kept
-//            in place at the front of the row's own product slots; count nonzero sums.
-//   stage 3  block scan of row counts, look-back for the tile's global offset, rows' entries
-//            staged in LDS in final order, then written with coalesced stores.
-// Tiles whose entries/products exceed the LDS caps run a sequential exact path (scipy's dense
-// sums/next accumulator in LDS), so any input is handled.
+// Pipelines (rp_project_plan reports which one a launch runs):
+//   row-lane (lpr_*, short rows over a packed R, the KDD2012 default): tiles of 256 rows, one wave
+//     per 64 rows, one flat pass per wave builds its rows' output in a fixed LDS slot in
+//     first-touch order (Bloom-flagged rows recomputed exactly), then one scan and one reversing
+//     copy place the slots. R descriptors come either straight from W (direct) or from the staged
+//     gather (count / run-scan / partition / gather kernels: bucket-major segments streamed
+//     against an L2-resident W32 slice); in auto mode lpr_choose_kernel picks one per call on the
+//     device. The staged main kernel is persistent and pipelines the next tile's loads.
+//   tile (spgemm_lookback_kernel, long rows / generic R): one workgroup per tile, products in LDS,
+//     first-touch leaders sum their column groups, decoupled look-back for the tile's offset,
+//     deferred output for tiles whose prefix is late (defer_copy_kernel).
+// Tiles past the LDS caps in either pipeline run scipy's dense sums/next accumulator exactly
+// (heavy_tile), so any input is handled.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -98,3 +98,21 @@ def test_invalid_r_rejected():
     R = sp.csr_matrix((np.ones(2, np.float32), np.array([0, 70]), np.array([0, 1, 2])), shape=(2, 64))
     with pytest.raises(nat.RPError, match="out of range"):
         pack(R)
+
+
+def test_documented_shape_limits():
+    """Limits scipy does not have, documented in DESIGN.md §7: p <= 32767 for any R on the GPU
+    path, and the packed layout only for p <= 16384 (a 15-bit slot: sign << 14 | column) — a
+    single-magnitude R with wider p falls back to the generic layout, and RP_LAYOUT_PACKED then
+    refuses it."""
+    R = sp.csr_matrix((np.ones(2, np.float32), np.array([0, 40000]), np.array([0, 1, 2])), shape=(2, 40000))
+    with pytest.raises(nat.RPError, match="32767"):
+        pack(R)
+    R = sp.csr_matrix((np.full(2, 0.5, np.float32), np.array([0, 19999]), np.array([0, 1, 2])), shape=(2, 20000))
+    info, _ = pack(R)
+    assert info.layout == nat.RP_LAYOUT_GENERIC
+    with pytest.raises(nat.RPError, match="packed"):
+        pack(R, nat.RP_LAYOUT_PACKED)
+    R = sp.csr_matrix((np.full(2, 0.5, np.float32), np.array([0, 16383]), np.array([0, 1, 2])), shape=(2, 16384))
+    info, _ = pack(R)
+    assert info.layout == nat.RP_LAYOUT_PACKED
