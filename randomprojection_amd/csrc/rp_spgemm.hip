@@ -1583,17 +1583,23 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             carry_k += __builtin_amdgcn_readlane(kinc, 63);
             carry_r += (uint32_t)__builtin_popcountll(fw);
         };
-        // values straight from HBM in entry order (coalesced), kXP steps in flight ahead of use
-        for (uint32_t j = 0; j < nsteps; j += kXP) {
-            T c[kXP];
+        // values straight from HBM in entry order (coalesced), kXP steps in flight ahead of use, in
+        // two alternating register sets: no copy at the loop edge, so a step waits only for the
+        // loads issued a half-iteration earlier (a copy there made every iteration wait for the
+        // loads it had just issued)
+        for (uint32_t j = 0; j < nsteps; j += 2 * kXP) {
+            T xw[kXP];
 #pragma unroll
-            for (int u = 0; u < kXP; ++u) {
-                c[u] = xv[u];
-                xv[u] = ldx(j + kXP + u);
-            }
+            for (int u = 0; u < kXP; ++u) xw[u] = ldx(j + kXP + u);
 #pragma unroll
             for (int u = 0; u < kXP; ++u)
-                if (j + u < nsteps) step(j + u, c[u]);
+                if (j + u < nsteps) step(j + u, xv[u]);
+            if (j + kXP >= nsteps) break;  // uniform
+#pragma unroll
+            for (int u = 0; u < kXP; ++u) xv[u] = ldx(j + 2 * kXP + u);
+#pragma unroll
+            for (int u = 0; u < kXP; ++u)
+                if (j + kXP + u < nsteps) step(j + kXP + u, xw[u]);
         }
         bool overflow = carry_k > sp.slot;
         __syncthreads();
@@ -1995,17 +2001,23 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
         carry_k += __builtin_amdgcn_readlane(kinc, 63);
         carry_r += (uint32_t)__builtin_popcountll(fw);
     };
-    // values straight from HBM in entry order (coalesced), four steps in flight ahead of use
-    for (uint32_t j = 0; j < nsteps; j += 4) {
-        T c0 = x0, c1 = x1, c2 = x2, c3 = x3;
-        x0 = ldx(j + 4);
-        x1 = ldx(j + 5);
-        x2 = ldx(j + 6);
-        x3 = ldx(j + 7);
-        step(j, c0);
-        if (j + 1 < nsteps) step(j + 1, c1);
-        if (j + 2 < nsteps) step(j + 2, c2);
-        if (j + 3 < nsteps) step(j + 3, c3);
+    // values straight from HBM in entry order (coalesced), four steps in flight ahead of use, in
+    // two alternating register sets (no copy at the loop edge: see lpr_main_kernel)
+    for (uint32_t j = 0; j < nsteps; j += 8) {
+        const T y0 = ldx(j + 4), y1 = ldx(j + 5), y2 = ldx(j + 6), y3 = ldx(j + 7);
+        step(j, x0);
+        if (j + 1 < nsteps) step(j + 1, x1);
+        if (j + 2 < nsteps) step(j + 2, x2);
+        if (j + 3 < nsteps) step(j + 3, x3);
+        if (j + 4 >= nsteps) break;  // uniform
+        x0 = ldx(j + 8);
+        x1 = ldx(j + 9);
+        x2 = ldx(j + 10);
+        x3 = ldx(j + 11);
+        step(j + 4, y0);
+        if (j + 5 < nsteps) step(j + 5, y1);
+        if (j + 6 < nsteps) step(j + 6, y2);
+        if (j + 7 < nsteps) step(j + 7, y3);
     }
     bool overflow = carry_k > sp.slot;
     __syncthreads();
