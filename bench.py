@@ -422,7 +422,7 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax):
         "dtype": "f32", "data": cfg["data"].format(dist=args.dist, p=args.p),
         "config": {"workload": "configs[1] host boundary: " + cfg["workload"].format(rows=n, m=args.m, p=args.p)
                                .replace("device-resident CSR in/out", "host CSR in/out"),
-                   "boundary": "host", "host_mem": args.host_mem, "chunk_rows": args.chunk_rows or 4 << 20,
+                   "boundary": "host", "host_mem": args.host_mem, "chunk_rows": args.chunk_rows or 2 << 20,
                    "nnz_in": nnz_a, "nnz_out": nnz_c, "order": order},
         "pcie": {"h2d_bytes": h2d, "d2h_bytes": d2h, "h2d_GBps": h2d / dt / 1e9, "d2h_GBps": d2h / dt / 1e9,
                  "link_peak_GBps_per_direction": 63.0, "measured_copy_GBps": "H2D ~55, D2H 48-55 concurrently "

@@ -200,7 +200,7 @@ int rp_project(rp_projector* h, const rp_csr_in* a_host, int32_t order, rp_alloc
 
 /* Chunked host streaming (boundary 2): C = A @ R for host CSR A of any size into caller host
  * arrays c_host (indptr: n_rows + 1 entries of indptr_type; indices/data: capacity entries; data in
- * the compute type). Rows go in chunks of chunk_rows (0 = 4M): chunk k+1's upload, chunk k's
+ * the compute type). Rows go in chunks of chunk_rows (0 = 2M): chunk k+1's upload, chunk k's
  * kernels and chunk k-1's download overlap (an upload thread, a download thread, a compute
  * stream; device output offsets chained on the device). Host arrays may be pageable or pinned
  * (rp_host_alloc: the copies then run without blocking their threads); pageable destinations

@@ -1273,6 +1273,7 @@ __device__ __forceinline__ T wave_incl_scan_t(T v, int lane) {
 // staged runs of the row-lane pipeline (see lpr_partition_kernel)
 struct LprStage {
     const uint32_t* gate;  // non-NULL: staged iff *gate (lpr_choose_kernel); the direct kernel iff !*gate
+    const uint32_t* w32;   // direct gathers from the 4-byte W32 table (NULL: the 8-byte W words)
     const uint16_t* offt;
     const uint32_t* off2;
     const int64_t* gb;
@@ -1919,12 +1920,24 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
                 const uint32_t e = q0 + u * kLprRows;
                 jv[u] = e < ne ? Ajt[e] : -1;
             }
-            uint64_t w[kU];
+            if (stg.w32) {  // the 4-byte W32 words: twice the features per line; > 2 entries -> side
+                uint32_t w[kU];
 #pragma unroll
-            for (int u = 0; u < kU; ++u) w[u] = jv[u] >= 0 ? R.W[jv[u]] : 0ull;
+                for (int u = 0; u < kU; ++u) w[u] = jv[u] >= 0 ? stg.w32[jv[u]] : 0u;
 #pragma unroll
-            for (int u = 0; u < kU; ++u)
-                if (q0 + u * kLprRows < ne) put_desc(q0 + u * kLprRows, w[u]);
+                for (int u = 0; u < kU; ++u)
+                    if (q0 + u * kLprRows < ne) {
+                        if ((w[u] >> 30) == 3) put_side(q0 + u * kLprRows, (w[u] >> 26) & 15u, w[u] & kW32J, 0ull, false);
+                        else s_desc[q0 + u * kLprRows] = w[u];
+                    }
+            } else {
+                uint64_t w[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) w[u] = jv[u] >= 0 ? R.W[jv[u]] : 0ull;
+#pragma unroll
+                for (int u = 0; u < kU; ++u)
+                    if (q0 + u * kLprRows < ne) put_desc(q0 + u * kLprRows, w[u]);
+            }
         }
     }
     if (tid <= nrows) s_rowptr[tid] = (uint16_t)(rp0 - ea);
@@ -1940,7 +1953,8 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     // pass (their counts came with the staged words), so this latency hides behind the pass
     const uint32_t nside = s_nside;
     uint64_t sidew = 0;
-    if (STAGED && (uint32_t)tid < nside) sidew = R.W[s_sidej[tid]];
+    const bool side_later = STAGED || stg.w32 != nullptr;  // side W words not in LDS yet
+    if (side_later && (uint32_t)tid < nside) sidew = R.W[s_sidej[tid]];
     // ---- step B: one wave per 64 rows, one flat pass over the wave's entries
     const int w = tid >> 6, lane = tid & 63;
     const int r = tid;  // this lane's row (for per-row work)
@@ -2023,8 +2037,8 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     __syncthreads();
     // side fill: every side entry's products into its gap, in R's storage order
     if ((uint32_t)tid < nside) {
-        const uint64_t sw = STAGED ? sidew : s_side[tid];
-        if (STAGED) s_side[tid] = sw;
+        const uint64_t sw = side_later ? sidew : s_side[tid];
+        if (side_later) s_side[tid] = sw;
         const uint32_t k0 = s_sfk[tid];
         if (k0 != 0xffffu) {
             uint16_t* cbw = s_colbuf + (size_t)s_sfw[tid] * sp.slot;
@@ -2544,6 +2558,9 @@ constexpr int kDeferPollsShort = 8;            // ... and before a tile of fewer
 constexpr int kDeferTicks = 800;               // 256-row tiles: wait budget, 8 us (defer_ticks_setting)
 constexpr bool kStageAuto = false;              // auto picks staging (off until it measures faster)
 constexpr int64_t kStageMinNnz = 1 << 22;      // auto: stage only launches this large
+// rp_project_stream's default chunk: configs[1] host CSR in/out measured 475 M rows/s with 4M-row
+// chunks, 544 M with 2M (shorter fill and drain of the upload/compute/download pipeline)
+constexpr int64_t kStreamChunkRows = (int64_t)2 << 20;
 constexpr int64_t kStageMinTable = 64ll << 20;  // ... and only a W past L2/MALL-friendly sizes
 
 // Row-lane pipeline choice: packed R, short rows (one lane walks a row), few products per row.
@@ -2780,7 +2797,7 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
                            (const uint32_t*)h->BM.p, (const int64_t*)GB, pl.sb, pl.nb, pl.groups,
                            (const uint32_t*)Sw, Dw, gate);
         HIP_TRY(hipGetLastError());
-        stg = LprStage{gate, OFFT, OFF2, GB, Sw, Dw, pl.ostride, pl.nb};
+        stg = LprStage{gate, nullptr, OFFT, OFF2, GB, Sw, Dw, pl.ostride, pl.nb};
     }
     const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot, pl.staged);
     // persistent grid: as many workgroups as can be resident (a multiple of 8: each stays in its
@@ -2801,6 +2818,8 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
                            a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
     }
     if (!pl.staged || pl.gated) {  // direct gathers (gated: runs iff the device chose them)
+        static const bool w64 = getenv("RP_LPR_DIRECT_W64") != nullptr;  // measurements
+        stg.w32 = w64 ? nullptr : (const uint32_t*)h->W32.p;
         const void* fn = (const void*)lpr_main_flat_kernel<T, IP, false>;
         HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL((lpr_main_flat_kernel<T, IP, false>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag,
@@ -3866,7 +3885,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
     if (a->n_rows < 0 || !a->indptr || !c->indptr) return fail(RP_ERR_INVALID, "bad CSR arrays");
     if (c->capacity > 0 && (!c->indices || !c->data)) return fail(RP_ERR_INVALID, "NULL output arrays");
     const int64_t n = a->n_rows;
-    if (chunk_rows <= 0) chunk_rows = 4 << 20;
+    if (chunk_rows <= 0) chunk_rows = kStreamChunkRows;
     // chunk plan from indptr at chunk boundaries (the rows inside a chunk are checked on the device)
     std::vector<StreamChunk> chunks;
     const int64_t b0 = ptr_at(a->indptr, a->indptr_type, 0);

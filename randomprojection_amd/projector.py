@@ -191,7 +191,7 @@ class Projector:
 
     def project_stream(self, indptr, indices, data, order: str = "scipy", chunk_rows: int = 0, out=None,
                        out_index_dtype=None, _index_rule_arrays=None):
-        """Host CSR in -> host CSR out through ``rp_project_stream``: rows in chunks (default 4M)
+        """Host CSR in -> host CSR out through ``rp_project_stream``: rows in chunks (default 2M)
         whose upload, projection and download overlap (boundary 2, BASELINE configs[1]'s chunked
         row streaming). ``out``: optional ``(indptr, indices, data)`` host arrays to fill (reused
         buffers avoid first-touch page faults; capacity = len(indices)); else recycled host memory
