@@ -10,9 +10,9 @@ for c in bf16 fp32; do
   i=0
   for pmc in "MfmaUtil" "MfmaFlopsBF16 MfmaFlopsF32"; do
     i=$((i+1))
-    timeout -s KILL 240 rocprofv3 --pmc $pmc -T --output-format csv -d gpurun_out/dense_pmc_${c}_$i -o pmc -- python3 scripts/bench_dense.py --compute $c --steps 3 --warmup 1 > gpurun_out/dense_pmc_${c}_$i.log 2>&1 || { tail -20 gpurun_out/dense_pmc_${c}_$i.log; exit 6; }
+    timeout -s KILL 240 rocprofv3 --pmc $pmc -T --output-format csv -d gpurun_out/dense_pmc_${c}_$i -o pmc -- python3 scripts/bench_dense.py --compute $c --steps 3 --warmup 1 --no-stream > gpurun_out/dense_pmc_${c}_$i.log 2>&1 || { tail -20 gpurun_out/dense_pmc_${c}_$i.log; exit 6; }
   done
-  timeout -s KILL 240 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/dense_trace_$c -o t -- python3 scripts/bench_dense.py --compute $c --steps 3 --warmup 1 > gpurun_out/dense_trace_$c.log 2>&1 || { tail -20 gpurun_out/dense_trace_$c.log; exit 7; }
+  timeout -s KILL 240 rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/dense_trace_$c -o t -- python3 scripts/bench_dense.py --compute $c --steps 3 --warmup 1 --no-stream > gpurun_out/dense_trace_$c.log 2>&1 || { tail -20 gpurun_out/dense_trace_$c.log; exit 7; }
   python3 scripts/pmc_kernels.py gpurun_out/dense_pmc_${c}_ > gpurun_out/dense_pmc_$c.json
 done
 echo done
