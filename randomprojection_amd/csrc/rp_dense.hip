@@ -94,7 +94,7 @@ struct DenseStep<float> {
 // two LDS buffers, the next step loaded to registers during the MFMAs and written to the other
 // buffer (one barrier per step); STAGES = 1: one buffer, written after a barrier (half the LDS,
 // so twice the blocks per CU). Rows past M / N are read as zeros and not stored.
-template <typename T, int WM, int WN, int TM, int TN, int STAGES>
+template <typename T, int WM, int WN, int TM, int TN, int STAGES, int DEPTH = 1>
 __global__ void __launch_bounds__(64 * WM * WN)
 dense_nt_kernel(const T* __restrict__ A, const T* __restrict__ B, float* __restrict__ C, int64_t M, int N, int K,
                 int64_t ldc, unsigned m_tiles, unsigned n_tiles) {
@@ -129,20 +129,22 @@ dense_nt_kernel(const T* __restrict__ A, const T* __restrict__ B, float* __restr
         gb[q] = reinterpret_cast<const char*>(B + (int64_t)(vb[q] ? rb : 0) * K) + sch * 16;
     }
     uint4 ra[PA], rb[PB];
-    auto load = [&](int s) {
+    auto load_to = [&](uint4 (&xa)[PA], uint4 (&xb)[PB], int s) {
         const int64_t off = (int64_t)s * kRowBytes;
 #pragma unroll
-        for (int q = 0; q < PA; ++q) ra[q] = *reinterpret_cast<const uint4*>(ga[q] + off);
+        for (int q = 0; q < PA; ++q) xa[q] = *reinterpret_cast<const uint4*>(ga[q] + off);
 #pragma unroll
-        for (int q = 0; q < PB; ++q) rb[q] = *reinterpret_cast<const uint4*>(gb[q] + off);
+        for (int q = 0; q < PB; ++q) xb[q] = *reinterpret_cast<const uint4*>(gb[q] + off);
     };
-    auto store = [&](int buf) {
+    auto store_from = [&](const uint4 (&xa)[PA], const uint4 (&xb)[PB], int buf) {
         const uint4 z = make_uint4(0, 0, 0, 0);
 #pragma unroll
-        for (int q = 0; q < PA; ++q) lds[buf][swz(srow + RPP * q, sch)] = va[q] ? ra[q] : z;
+        for (int q = 0; q < PA; ++q) lds[buf][swz(srow + RPP * q, sch)] = va[q] ? xa[q] : z;
 #pragma unroll
-        for (int q = 0; q < PB; ++q) lds[buf][BM * 8 + swz(srow + RPP * q, sch)] = vb[q] ? rb[q] : z;
+        for (int q = 0; q < PB; ++q) lds[buf][BM * 8 + swz(srow + RPP * q, sch)] = vb[q] ? xb[q] : z;
     };
+    auto load = [&](int s) { load_to(ra, rb, s); };
+    auto store = [&](int buf) { store_from(ra, rb, buf); };
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int a = 0; a < TM; ++a)
@@ -151,6 +153,26 @@ dense_nt_kernel(const T* __restrict__ A, const T* __restrict__ B, float* __restr
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
     const int ra0 = wm * TM * 32, rb0 = wn * TN * 32;
+    if constexpr (DEPTH == 2 && STAGES == 2) {
+        // two register sets, each step's tiles loaded two steps ahead (no copies between the sets):
+        // step s computes from LDS buffer s & 1 while its successor's registers are already loaded
+        uint4 ra2[PA], rb2[PB];
+        load(0);
+        store(0);
+        __syncthreads();
+        if (steps > 1) load(1);
+        for (int s = 0; s < steps; s += 2) {
+            if (s + 2 < steps) load_to(ra2, rb2, s + 2);
+            DenseStep<T>::template compute<TM, TN>(lds[0], lds[0] + BM * 8, ra0, rb0, lane, acc);
+            if (s + 1 < steps) store(1);
+            __syncthreads();
+            if (s + 1 >= steps) break;
+            if (s + 3 < steps) load(s + 3);
+            DenseStep<T>::template compute<TM, TN>(lds[1], lds[1] + BM * 8, ra0, rb0, lane, acc);
+            if (s + 2 < steps) store_from(ra2, rb2, 0);
+            __syncthreads();
+        }
+    } else {
     load(0);
     store(0);
     __syncthreads();
@@ -166,6 +188,7 @@ dense_nt_kernel(const T* __restrict__ A, const T* __restrict__ B, float* __restr
             if (s + 1 < steps) store(0);
             __syncthreads();
         }
+    }
     }
     // epilogue: lane holds column lane & 31 of each 32 x 32 tile, rows
     // (e & 3) + 8 (e >> 2) + 4 (lane >> 5) for e < 16
@@ -184,14 +207,14 @@ dense_nt_kernel(const T* __restrict__ A, const T* __restrict__ B, float* __restr
         }
 }
 
-template <typename T, int WM, int WN, int TM, int TN, int STAGES>
+template <typename T, int WM, int WN, int TM, int TN, int STAGES, int DEPTH = 1>
 int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
                  hipStream_t st) {
     constexpr int BM = WM * TM * 32, BN = WN * TN * 32;
     const unsigned m_tiles = (unsigned)((n + BM - 1) / BM), n_tiles = (unsigned)((p + BN - 1) / BN);
     const uint64_t blocks = (uint64_t)((m_tiles + 7) / 8) * 8ull * n_tiles;
     if (blocks >= (1ull << 31)) return fail(RP_ERR_UNSUPPORTED, "too many rows for one launch");
-    hipLaunchKernelGGL((dense_nt_kernel<T, WM, WN, TM, TN, STAGES>), dim3((unsigned)blocks), dim3(64 * WM * WN), 0,
+    hipLaunchKernelGGL((dense_nt_kernel<T, WM, WN, TM, TN, STAGES, DEPTH>), dim3((unsigned)blocks), dim3(64 * WM * WN), 0,
                        st, (const T*)X, (const T*)G, Y, n, (int)p, (int)m, ldy, m_tiles, n_tiles);
     HIP_TRY(hipGetLastError());
     return RP_OK;
@@ -210,6 +233,10 @@ int dispatch_dense(int v, const void* X, const void* G, float* Y, int64_t n, int
         case 3: return launch_dense<T, 2, 4, 2, 2, 2>(X, G, Y, n, m, p, ldy, st);
         case 4: return launch_dense<T, 2, 4, 4, 2, 1>(X, G, Y, n, m, p, ldy, st);
         case 5: return launch_dense<T, 2, 4, 4, 2, 2>(X, G, Y, n, m, p, ldy, st);
+        case 6: return launch_dense<T, 2, 4, 4, 2, 2, 2>(X, G, Y, n, m, p, ldy, st);
+        case 7: return launch_dense<T, 2, 2, 2, 2, 2, 2>(X, G, Y, n, m, p, ldy, st);
+        case 8: return launch_dense<T, 2, 2, 4, 4, 2, 2>(X, G, Y, n, m, p, ldy, st);
+        case 9: return launch_dense<T, 2, 2, 4, 4, 2, 1>(X, G, Y, n, m, p, ldy, st);
         default: return launch_dense<T, 2, 2, 2, 2, 2>(X, G, Y, n, m, p, ldy, st);
     }
 }
