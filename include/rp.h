@@ -19,8 +19,11 @@
  *      projected_features = features_matrix.dot(local_csr_matrix)
  *                                                        code/clustermode/randomProjection.py:46
  *      -> scipy _sparsetools.csr_matmat_maxnnz + csr_matmat  scipy/sparse/_compressed.py:569-595
- *    Device-resident CSR in, device-resident CSR out, one kernel launch (single pass: count, scan
- *    via decoupled look-back, fill). Output equals scipy's bit for bit: same per-row order
+ *    Device-resident CSR in, device-resident CSR out, asynchronous on one stream. The call runs one
+ *    of two kernel pipelines (rp_project_plan): the row-lane pipeline for short rows over a packed
+ *    R (KDD2012; up to 11 kernels: staged-gather count/scan/partition/gather, main, heavy-tile,
+ *    scan, copy) or the tile pipeline for long rows / generic R (one look-back kernel + a copy of
+ *    deferred tiles). Output equals scipy's bit for bit: same per-row order
  *    (RP_ORDER_SCIPY = reverse first-touch) or ascending (RP_ORDER_SORTED = what pyspark's
  *    SparseVector makes of it, code/clustermode/randomProjection.py:49-50), same zero drop, values
  *    computed with the same separately rounded multiply and add.
@@ -154,6 +157,28 @@ int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_
  * bucket_shift: 2^shift features per bucket (0 = auto, 19). Results are identical either way. */
 int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift);
 
+/* Per-projector tuning and test options (the library reads no environment variables). Results are
+ * identical under every setting; only the schedule changes. value < default sentinel restores the
+ * default.
+ *   RP_OPT_PIPELINE      0 auto (default); 1 tile pipeline; 2 row-lane pipeline where it can run
+ *   RP_OPT_DEFER_POLLS   tile pipeline: -2 default (time budget); -1 tiles never park their output;
+ *                        n >= 0 park after n unsuccessful look-back polls (time budget off)
+ *   RP_OPT_DEFER_TICKS   256-row tiles' look-back wait budget in s_memrealtime ticks (100 MHz):
+ *                        -1 default (800 = 8 us); n >= 0 override
+ *   RP_OPT_CHUNK_ROWS    row-lane rows per launch sequence: 0 default (2^27), else rounded up to
+ *                        whole 256-row tiles
+ *   RP_OPT_HOST_THREADS  helper threads of the host result download: -1 default (min(4, cores));
+ *                        0 or 1 plain copies */
+typedef enum {
+    RP_OPT_PIPELINE = 1,
+    RP_OPT_DEFER_POLLS = 2,
+    RP_OPT_DEFER_TICKS = 3,
+    RP_OPT_CHUNK_ROWS = 4,
+    RP_OPT_HOST_THREADS = 5
+} rp_option;
+int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value);
+int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* value);
+
 /* The kernel pipeline rp_project_device would run for n_rows rows holding nnz_a entries with the
  * full workspace: *pipeline = RP_PIPE_TILE (one-launch tile SpGEMM with look-back) or
  * RP_PIPE_ROWLANE (row-lane kernel: short rows over a packed R), *staged = 1 if the R descriptors
@@ -164,9 +189,11 @@ typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1 } rp_pipeline;
 int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t* pipeline, int32_t* staged,
                     int32_t* bucket_shift);
 
-/* After a completed rp_project_device call with `workspace` on n_rows / nnz_a: *staged = 1 if that
- * call used the staged gather, 0 if direct gathers (rp_project_plan's *staged == 2: decided on the
- * device per call, from a sample of the input's feature ids). Synchronous (4-byte copy). */
+/* After an rp_project_device call with `workspace` has completed (its stream synchronised by the
+ * caller): *staged = 1 if that call used the staged gather, 0 if direct gathers (rp_project_plan's
+ * *staged == 2: decided on the device per call, from a sample of the input's feature ids). The
+ * call records what actually ran in the workspace header, so a re-planned call (a workspace too
+ * small for staging) reads 0. n_rows / nnz_a are unused (kept for the ABI). 4-byte copy. */
 int rp_project_choice(const rp_projector* h, int64_t n_rows, int64_t nnz_a, const void* workspace,
                       int32_t* staged);
 
@@ -244,6 +271,8 @@ int rp_libsvm_parse_device(int device, const char* text, int64_t n_bytes, int64_
  * (sklearn/random_projection.py:569-612) with a hand-written MFMA GEMM. Asynchronous on `stream`. */
 int rp_dense_project_device(int device, const void* X, int32_t dtype, int64_t n, int64_t m, const void* G,
                             int64_t p, float* Y, int64_t ldy, void* stream);
+/* Library-wide tile variant of rp_dense_project_device (measurements): -1 = the default. */
+int rp_dense_set_variant(int32_t variant);
 
 #ifdef __cplusplus
 }

@@ -16,16 +16,18 @@ RP_OK, RP_ERR_INVALID, RP_ERR_HIP, RP_ERR_CAPACITY, RP_ERR_UNSUPPORTED, RP_ERR_N
 RP_I32, RP_I64, RP_F32, RP_F64, RP_BF16 = 1, 2, 3, 4, 5
 RP_LAYOUT_AUTO, RP_LAYOUT_GENERIC, RP_LAYOUT_PACKED = 0, 1, 2
 RP_ORDER_SCIPY, RP_ORDER_SORTED = 0, 1
+RP_OPT_PIPELINE, RP_OPT_DEFER_POLLS, RP_OPT_DEFER_TICKS, RP_OPT_CHUNK_ROWS, RP_OPT_HOST_THREADS = 1, 2, 3, 4, 5
 
 # every symbol include/rp.h declares (tests/test_abi.py checks the .so exports them all)
 EXPORTS = (
     "rp_last_error", "rp_version", "rp_device_count",
     "rp_projector_create", "rp_projector_info_get", "rp_projector_export",
     "rp_projector_create_from_device", "rp_projector_destroy", "rp_pack_r_host",
-    "rp_project_workspace_bytes", "rp_project_plan", "rp_project_choice", "rp_projector_set_staging", "rp_project_device",
+    "rp_project_workspace_bytes", "rp_project_plan", "rp_project_choice", "rp_projector_set_staging",
+    "rp_projector_set_option", "rp_projector_get_option", "rp_project_device",
     "rp_project_host_begin", "rp_result_fetch", "rp_result_free", "rp_project",
     "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_project_stream", "rp_host_alloc", "rp_host_free",
-    "rp_dense_project_device",
+    "rp_dense_project_device", "rp_dense_set_variant",
 )
 
 
@@ -110,6 +112,8 @@ def load(path: str = None):
         "rp_project_plan": (ctypes.c_int, [vp, i64, i64, P(i32), P(i32), P(i32)]),
         "rp_project_choice": (ctypes.c_int, [vp, i64, i64, vp, P(i32)]),
         "rp_projector_set_staging": (ctypes.c_int, [vp, i32, i32]),
+        "rp_projector_set_option": (ctypes.c_int, [vp, i32, i64]),
+        "rp_projector_get_option": (ctypes.c_int, [vp, i32, P(i64)]),
         "rp_project_device": (ctypes.c_int, [vp, P(CsrIn), P(CsrOut), i32, vp, i64, vp, P(i64)]),
         "rp_project_host_begin": (ctypes.c_int, [vp, P(CsrIn), i32, P(vp), P(i64)]),
         "rp_result_fetch": (ctypes.c_int, [vp, vp, i32, vp, i32, vp]),
@@ -121,6 +125,7 @@ def load(path: str = None):
         "rp_synth_rows_device": (ctypes.c_int, [ctypes.c_int, i64, i64, dbl, i32, i32, dbl, ctypes.c_uint64,
                                                 vp, i32, vp, vp, vp, P(i64)]),
         "rp_dense_project_device": (ctypes.c_int, [ctypes.c_int, vp, i32, i64, i64, vp, i64, vp, i64, vp]),
+        "rp_dense_set_variant": (ctypes.c_int, [i32]),
         "rp_libsvm_parse_device": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, vp, vp, i32, vp, vp, i64, i64, vp,
                                                   P(i64), P(i64), P(i64)]),
     }

@@ -1,6 +1,7 @@
 """Build librp.so (HIP, gfx950) in-tree with hipcc. No CUDA, no hipify, no multi-target build."""
 from __future__ import annotations
 
+import fcntl
 import os
 import subprocess
 import sys
@@ -33,26 +34,35 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
     used only by scripts/stage_stamps.py, never by the package. Sources compile in parallel (one
     hipcc per .hip into build/), then link."""
     out = DIAG_OUT if diag else OUT
-    if force or diag or needs_build():
-        extra = ["-DRP_STAMPS"] if diag else []
-        odir = os.path.join(HERE, "build", "diag" if diag else "rel")
-        os.makedirs(odir, exist_ok=True)
-        objs, procs = [], []
-        for src in SRC:
-            obj = os.path.join(odir, os.path.basename(src) + ".o")
-            cmd = [HIPCC, *[f for f in FLAGS if f != "-shared"], *extra, "-c", "-o", obj, src]
-            if verbose:
-                print(" ".join(cmd), file=sys.stderr)
-            objs.append(obj)
-            procs.append(subprocess.Popen(cmd))
-        if any(p.wait() != 0 for p in procs):
-            raise subprocess.CalledProcessError(1, "hipcc")
-        cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
+    os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
+    # one build at a time (two importers racing on the same objects); re-check under the lock
+    with open(os.path.join(HERE, "build", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if force or diag or needs_build():
+            _compile_and_link(out, diag, verbose)
+    return out
+
+
+def _compile_and_link(out: str, diag: bool, verbose: bool) -> None:
+    extra = ["-DRP_STAMPS"] if diag else []
+    odir = os.path.join(HERE, "build", "diag" if diag else "rel")
+    os.makedirs(odir, exist_ok=True)
+    objs, procs = [], []
+    for src in SRC:
+        obj = os.path.join(odir, os.path.basename(src) + ".o")
+        cmd = [HIPCC, *[f for f in FLAGS if f != "-shared"], *extra, "-c", "-o", obj, src]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
-        os.replace(out + ".tmp", out)
-    return out
+        objs.append(obj)
+        procs.append(subprocess.Popen(cmd))
+    rcs = [p.wait() for p in procs]  # every compile finishes before any failure is raised
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs), "hipcc")
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
 
 
 if __name__ == "__main__":

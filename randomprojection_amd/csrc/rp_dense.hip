@@ -19,6 +19,8 @@
 // Block -> tile map is XCD-aware: XCD x (workgroup i runs on XCD i % 8) takes the M tiles
 // congruent to x mod 8 and walks each M tile's N tiles back to back, so an X tile is fetched from
 // HBM once and re-read from that XCD's L2.
+#include <atomic>
+
 #include "rp_common.h"
 
 using namespace rpd;
@@ -241,7 +243,15 @@ int dispatch_dense(int v, const void* X, const void* G, float* Y, int64_t n, int
     }
 }
 
+std::atomic<int> g_dense_variant{-1};  // rp_dense_set_variant (measurements); -1 = kDenseVariant
+
 }  // namespace
+
+extern "C" int rp_dense_set_variant(int32_t variant) {
+    if (variant < -1 || variant > 7) return fail(RP_ERR_INVALID, "variant must be -1 (default) or 0..7");
+    g_dense_variant.store(variant, std::memory_order_relaxed);
+    return RP_OK;
+}
 
 extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype, int64_t n, int64_t m,
                                        const void* G, int64_t p, float* Y, int64_t ldy, void* stream) {
@@ -255,8 +265,8 @@ extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype,
     if (al & 15) return fail(RP_ERR_INVALID, "X and G must be 16-byte aligned");
     if (n == 0) return RP_OK;
     HIP_TRY(hipSetDevice(device));
-    const char* e = getenv("RP_DENSE_VARIANT");
-    const int v = e ? atoi(e) : kDenseVariant;
+    const int sv = g_dense_variant.load(std::memory_order_relaxed);
+    const int v = sv >= 0 ? sv : kDenseVariant;
     hipStream_t st = (hipStream_t)stream;
     return dtype == RP_BF16 ? dispatch_dense<uint16_t>(v, X, G, Y, n, m, p, ldy, st)
                             : dispatch_dense<float>(v, X, G, Y, n, m, p, ldy, st);

@@ -77,7 +77,7 @@ struct Workspace {              // device memory header; tile states follow at +
     unsigned int error;
     unsigned long long total;
     unsigned int n_deferred;    // tiles that parked their output in the pool (see defer below)
-    unsigned int pad0;
+    unsigned int staged_used;   // written last in a call: 1 = the staged gather ran (rp_project_choice)
     unsigned long long pool_used;  // entries of the deferred-output pool handed out
     unsigned long long pad[4];
 };
@@ -2483,6 +2483,12 @@ struct rp_projector {
     DevBuf BM;           // nonempty-feature bitmap (1 bit per feature) for the filtered gather
     int stage_mode = -1; // -1 auto, 0 off, 1 on (rp_projector_set_staging)
     int stage_sb = 0;    // bucket = 2^sb features; 0 = auto
+    // rp_projector_set_option (tuning and tests; the library reads no environment variables)
+    int opt_pipeline = 0;       // 0 auto, 1 tile, 2 row-lane where it can run
+    int opt_defer_polls = -2;   // -2 default (time budget), -1 never defer, n >= 0 polls
+    int opt_defer_ticks = -1;   // -1 default
+    int64_t opt_chunk_rows = 0; // 0 default
+    int opt_host_threads = -1;  // -1 default
     // generic
     DevBuf Bp, Bj, Bx32, Bx64;
     // internal workspace and host-path staging
@@ -2571,9 +2577,9 @@ constexpr bool kLprStageAuto = true;   // ... and staging inside it (large launc
 // rows per launch sequence of the row-lane pipeline: the workspace (~150 B per KDD2012 row) is sized
 // for one chunk, so a launch of 1.08B rows (configs[2] on one GPU) needs ~20 GB, not ~190 GB
 constexpr int64_t kLprChunkRows = (int64_t)1 << 27;
-int64_t lpr_chunk_rows() {  // RP_LPR_CHUNK_ROWS (tests): smaller chunks, rounded up to whole tiles
-    if (const char* e = getenv("RP_LPR_CHUNK_ROWS"))
-        return std::max<int64_t>(kLprRows, (atoll(e) + kLprRows - 1) / kLprRows * kLprRows);
+int64_t lpr_chunk_rows(const rp_projector* h) {  // RP_OPT_CHUNK_ROWS: rounded up to whole tiles
+    if (h->opt_chunk_rows > 0)
+        return std::max<int64_t>(kLprRows, (h->opt_chunk_rows + kLprRows - 1) / kLprRows * kLprRows);
     return kLprChunkRows;
 }
 bool lpr_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
@@ -2582,9 +2588,8 @@ bool lpr_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
     const double avg = (double)nnz_a / (double)n_rows;
     const bool fits = avg <= kLprMaxRowEntries && avg * ppe <= kLprMaxRowProducts &&
                       avg * kLprRows + 6.0 * std::sqrt(avg * kLprRows) + 40.0 <= kCapAMax;
-    const char* e = getenv("RP_PIPE");
-    if (e && !strcmp(e, "tile")) return false;
-    if (e && !strcmp(e, "lpr")) return fits;
+    if (h->opt_pipeline == 1) return false;  // RP_OPT_PIPELINE: tile forced
+    if (h->opt_pipeline == 2) return fits;   // row-lane forced where it can run
     return kLprAuto && fits;
 }
 
@@ -2606,7 +2611,7 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
         // mean + 7 sigma (sigma ~ 1.25 sqrt(mean) for single-magnitude SRP rows) + 32: KDD2012 608,
         // which keeps a tile's LDS (descriptors + the 4 slots) at 32 KB: 5 tiles per CU
         pl.lpr_slot = (uint32_t)std::min<double>(65535.0, ((int)(prods_w + 8.75 * std::sqrt(prods_w) + 32.0) + 31) & ~31);
-        pl.lpr_chunk = std::min<int64_t>(n_rows, lpr_chunk_rows());
+        pl.lpr_chunk = std::min<int64_t>(n_rows, lpr_chunk_rows(h));
         pl.n_tiles = (pl.lpr_chunk + kLprRows - 1) / kLprRows;
         const size_t nw = 4 * (size_t)pl.n_tiles;
         pl.scan_blocks = ((int64_t)nw + kBlock * kScanPer - 1) / (kBlock * kScanPer);
@@ -2697,16 +2702,16 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
 // waits fewer polls where predecessors are slow and more where they finish quickly. Measured
 // (DESIGN.md §3d): 8 us gives configs[1] uniform 27.95 ms (polls: 27.9 at best) and power-law
 // 19.4 ms (polls 4: 21.0, never deferring: 19.8); 12 us already costs uniform 29.1 ms.
-// RP_DEFER_POLLS (tests, tuning) turns the time budget off; RP_DEFER_TICKS overrides it.
-int defer_ticks_setting(const Caps& caps) {
-    if (const char* e = getenv("RP_DEFER_TICKS")) return std::max(atoi(e), 0);
-    if (getenv("RP_DEFER_POLLS")) return 0;
+// RP_OPT_DEFER_POLLS (tests, tuning) turns the time budget off; RP_OPT_DEFER_TICKS overrides it.
+int defer_ticks_setting(const rp_projector* h, const Caps& caps) {
+    if (h->opt_defer_ticks >= 0) return h->opt_defer_ticks;
+    if (h->opt_defer_polls >= -1) return 0;
     return caps.rpt >= 128 ? kDeferTicks : 0;
 }
 
-int defer_polls_setting(const Caps& caps) {
-    const char* e = getenv("RP_DEFER_POLLS");  // tests and tuning: -1 never defer, 0 defer at once
-    return e ? atoi(e) : (caps.rpt >= 128 ? kDeferPolls : kDeferPollsShort);
+int defer_polls_setting(const rp_projector* h, const Caps& caps) {
+    if (h->opt_defer_polls >= -1) return h->opt_defer_polls;  // -1 never defer, 0 defer at once
+    return caps.rpt >= 128 ? kDeferPolls : kDeferPollsShort;
 }
 
 template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED, int WPE = 1>
@@ -2719,8 +2724,6 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
             return launch_main<T, IP, OP, OI, RL, STAGED, 7>(R, mag, h, a, c, order, ws, n_tiles, pl, lds,
                                                              st, S, SX, D);
     }
-    if (const char* pad = STAGED ? nullptr : getenv("RP_DEBUG_LDS_PAD"))  // residency experiments
-        lds = std::min<size_t>(lds + (size_t)atol(pad), 160 * 1024 - 2048);
     HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED, WPE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     char* base = reinterpret_cast<char*>(ws);
@@ -2732,8 +2735,8 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
                        R, mag, (int)h->p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
                        (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order,
-                       ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting(pl.caps) : -1,
-                       pl.defer ? defer_ticks_setting(pl.caps) : 0);
+                       ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting(h, pl.caps) : -1,
+                       pl.defer ? defer_ticks_setting(h, pl.caps) : 0);
     HIP_TRY(hipGetLastError());
     if (pl.defer) {
         hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, kDeferCopyGrid)), dim3(kBlock), 0,
@@ -2818,8 +2821,7 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
                            a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
     }
     if (!pl.staged || pl.gated) {  // direct gathers (gated: runs iff the device chose them)
-        static const bool w64 = getenv("RP_LPR_DIRECT_W64") != nullptr;  // measurements
-        stg.w32 = w64 ? nullptr : (const uint32_t*)h->W32.p;
+        stg.w32 = (const uint32_t*)h->W32.p;
         const void* fn = (const void*)lpr_main_flat_kernel<T, IP, false>;
         HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL((lpr_main_flat_kernel<T, IP, false>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag,
@@ -3019,6 +3021,12 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
         rc = dispatch_idx<float, GenericR<float>>(R, 0.0f, h, a, c, order, ws, n_tiles, plan, lds, st);
     }
     if (rc) return rc;
+    // what ran, for rp_project_choice: the device's gate when it decided, else the plan's staging
+    if (plan.lpr && plan.gated)
+        HIP_TRY(hipMemcpyAsync(&ws->staged_used, reinterpret_cast<char*>(ws) + plan.carry + 16, 4,
+                               hipMemcpyDeviceToDevice, st));
+    else
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&ws->staged_used, plan.staged ? 1 : 0, 1, st));
     if (total_nnz) {
         Workspace hw;
         HIP_TRY(hipMemcpyAsync(&hw, ws, sizeof hw, hipMemcpyDeviceToHost, st));
@@ -3378,15 +3386,14 @@ int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_
 int rp_project_choice(const rp_projector* h, int64_t n_rows, int64_t nnz_a, const void* workspace,
                       int32_t* staged) {
     if (!h || !staged) return fail(RP_ERR_INVALID, "NULL argument");
-    const Plan pl = make_plan(h, n_rows, nnz_a);
-    if (!pl.gated) {
-        *staged = pl.staged ? 1 : 0;
-        return RP_OK;
-    }
+    (void)n_rows;
+    (void)nnz_a;
     if (!workspace) return fail(RP_ERR_INVALID, "the choice lives in the caller's workspace");
+    // every call records what ran in its workspace header (after all its kernels, on its stream);
+    // the caller has synchronised that stream (documented in rp.h)
     uint32_t g = 0;
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(hipMemcpy(&g, reinterpret_cast<const char*>(workspace) + pl.carry + 16, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&g, &reinterpret_cast<const Workspace*>(workspace)->staged_used, 4, hipMemcpyDeviceToHost));
     *staged = g ? 1 : 0;
     return RP_OK;
 }
@@ -3405,6 +3412,42 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
     h->stage_mode = mode;
     h->stage_sb = bucket_shift;
     return RP_OK;
+}
+
+int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value) {
+    if (!h) return fail(RP_ERR_INVALID, "NULL projector");
+    switch (option) {
+        case RP_OPT_PIPELINE:
+            if (value < 0 || value > 2) return fail(RP_ERR_INVALID, "pipeline must be 0 (auto), 1 (tile) or 2 (row-lane)");
+            h->opt_pipeline = (int)value;
+            return RP_OK;
+        case RP_OPT_DEFER_POLLS:
+            h->opt_defer_polls = (int)std::max<int64_t>(std::min<int64_t>(value, 1 << 30), -2);
+            return RP_OK;
+        case RP_OPT_DEFER_TICKS:
+            h->opt_defer_ticks = (int)std::max<int64_t>(std::min<int64_t>(value, 1 << 30), -1);
+            return RP_OK;
+        case RP_OPT_CHUNK_ROWS:
+            h->opt_chunk_rows = std::max<int64_t>(value, 0);
+            return RP_OK;
+        case RP_OPT_HOST_THREADS:
+            h->opt_host_threads = (int)std::max<int64_t>(std::min<int64_t>(value, 256), -1);
+            return RP_OK;
+        default:
+            return fail(RP_ERR_INVALID, "unknown option %d", option);
+    }
+}
+
+int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* value) {
+    if (!h || !value) return fail(RP_ERR_INVALID, "NULL argument");
+    switch (option) {
+        case RP_OPT_PIPELINE: *value = h->opt_pipeline; return RP_OK;
+        case RP_OPT_DEFER_POLLS: *value = h->opt_defer_polls; return RP_OK;
+        case RP_OPT_DEFER_TICKS: *value = h->opt_defer_ticks; return RP_OK;
+        case RP_OPT_CHUNK_ROWS: *value = h->opt_chunk_rows; return RP_OK;
+        case RP_OPT_HOST_THREADS: *value = h->opt_host_threads; return RP_OK;
+        default: return fail(RP_ERR_INVALID, "unknown option %d", option);
+    }
 }
 
 int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int32_t order,
@@ -3561,18 +3604,17 @@ struct D2HJob {
     size_t bytes;
 };
 
-unsigned host_threads() {
-    const char* e = getenv("RP_HOST_THREADS");  // 0/1: no helper threads
-    if (e) return (unsigned)std::max(0, atoi(e));
+unsigned host_threads(const rp_projector* h) {  // RP_OPT_HOST_THREADS; 0/1: no helper threads
+    if (h->opt_host_threads >= 0) return (unsigned)h->opt_host_threads;
     const unsigned hw = std::thread::hardware_concurrency();
     return std::min(4u, hw > 1 ? hw : 1u);
 }
 
-int fetch_d2h(const std::vector<D2HJob>& jobs) {
+int fetch_d2h(const rp_projector* h, const std::vector<D2HJob>& jobs) {
     constexpr size_t kChunk = 8u << 20, kPage = 4096, kMinPipelined = 16u << 20;
     size_t total = 0;
     for (const auto& j : jobs) total += j.bytes;
-    const unsigned nt = host_threads();
+    const unsigned nt = host_threads(h);
     if (total < kMinPipelined || nt < 2) {
         for (const auto& j : jobs)
             if (j.bytes) HIP_TRY(hipMemcpy(j.dst, j.src, j.bytes, hipMemcpyDeviceToHost));
@@ -3646,7 +3688,7 @@ int rp_result_fetch(rp_result* r, void* indptr, int32_t indptr_type, void* indic
         }
         jobs.push_back({data, r->cx.p, (size_t)dtype_size(r->value_type) * (size_t)r->nnz});
     }
-    return fetch_d2h(jobs);
+    return fetch_d2h(r->h, jobs);
 }
 
 int rp_result_free(rp_result* r) {
@@ -3698,13 +3740,15 @@ __global__ void stream_rebase_kernel(const IP* __restrict__ raw, int64_t* __rest
     }
 }
 
-// info[0] = this chunk's first output position (running total before it), info[1] = its nnz
+// info[0] = this chunk's first output position (running total before it), info[1] = its nnz,
+// info[4] = the chunk's device error word (a look-back wait that expired: its total is not valid)
 __global__ void stream_finish_kernel(const Workspace* __restrict__ ws, unsigned long long* __restrict__ total,
                                      unsigned long long* __restrict__ info) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         const unsigned long long b = *total, k = ws->total;
         info[0] = b;
         info[1] = k;
+        info[4] = ws->error;
         *total = b + k;
     }
 }
@@ -3721,7 +3765,7 @@ struct StreamSlot {
     DevBuf raw, ap, aj, ax;   // input chunk: indptr as given, rebased int64 indptr, indices, values
     DevBuf cp, cj, cx;        // output chunk: int64 chunk-relative indptr, int32 indices, values
     DevBuf optr, oidx;        // download forms: global indptr in the caller's type, int64 indices
-    DevBuf ws, info;          // workspace; info = {base, nnz, first bad column pos, first bad row}
+    DevBuf ws, info;          // workspace; info = {base, nnz, first bad column pos, first bad row, error}
     int64_t cap = 0;
     hipEvent_t comp = nullptr;
 };
@@ -3776,7 +3820,7 @@ int stream_compute(rp_projector* h, const rp_csr_in* a, const StreamChunk& ck, S
                    int ip_type, int vt,
                    int out_ip, int out_ix, unsigned long long* total, bool last, hipStream_t st) {
     unsigned long long* info = (unsigned long long*)s.info.p;
-    const unsigned long long init[4] = {0, 0, ~0ull, ~0ull};
+    const unsigned long long init[5] = {0, 0, ~0ull, ~0ull, 0};
     HIP_TRY(hipMemcpyAsync(info, init, sizeof init, hipMemcpyHostToDevice, st));
     const int64_t e_base = ck.e0;
     if (ip_type == RP_I64)
@@ -3827,9 +3871,10 @@ int stream_compute(rp_projector* h, const rp_csr_in* a, const StreamChunk& ck, S
 int stream_download(const StreamChunk& ck, StreamSlot& s, const rp_csr_in* a, const rp_csr_out* c, bool last,
                     hipStream_t st, int vs, int64_t* nnz_out, bool* redo) {
     HIP_TRY(hipEventSynchronize(s.comp));
-    unsigned long long info[4];
+    unsigned long long info[5];
     HIP_TRY(hipMemcpyAsync(info, s.info.p, sizeof info, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (info[4]) return fail(RP_ERR_TIMEOUT, "device look-back wait expired (rows %lld..)", (long long)ck.r0);
     const int64_t base = (int64_t)info[0], k = (int64_t)info[1];
     *nnz_out = k;
     const int ops = dtype_size(c->indptr_type), oxs = dtype_size(c->indices_type);

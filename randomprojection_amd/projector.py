@@ -14,6 +14,7 @@ There is no CPU fallback: a missing library or GPU raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import threading
 import weakref
@@ -329,6 +330,41 @@ class Projector:
         """Staged gather: "auto", "off" or "on" (identical results)."""
         code = {"auto": -1, "off": 0, "on": 1}[mode]
         nat.check(self._lib.rp_projector_set_staging(self._h, code, int(bucket_shift)))
+
+    _OPTIONS = {"pipeline": nat.RP_OPT_PIPELINE, "defer_polls": nat.RP_OPT_DEFER_POLLS,
+                "defer_ticks": nat.RP_OPT_DEFER_TICKS, "chunk_rows": nat.RP_OPT_CHUNK_ROWS,
+                "host_threads": nat.RP_OPT_HOST_THREADS}
+    _OPTION_DEFAULTS = {"pipeline": 0, "defer_polls": -2, "defer_ticks": -1, "chunk_rows": 0, "host_threads": -1}
+    _PIPELINES = {"auto": 0, "tile": 1, "rowlane": 2}
+
+    def set_option(self, name: str, value):
+        """Tuning / test option of this projector (rp_projector_set_option; results are identical
+        under every setting): pipeline ("auto" | "tile" | "rowlane"), defer_polls, defer_ticks,
+        chunk_rows, host_threads; ``None`` restores the default."""
+        if name not in self._OPTIONS:
+            raise ValueError(f"unknown option {name!r}; one of {sorted(self._OPTIONS)}")
+        if value is None:
+            value = self._OPTION_DEFAULTS[name]
+        elif name == "pipeline" and isinstance(value, str):
+            value = self._PIPELINES[value]
+        nat.check(self._lib.rp_projector_set_option(self._h, self._OPTIONS[name], int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = ctypes.c_int64()
+        nat.check(self._lib.rp_projector_get_option(self._h, self._OPTIONS[name], ctypes.byref(v)))
+        return int(v.value)
+
+    @contextlib.contextmanager
+    def options(self, **kw):
+        """Set options for the duration of a ``with`` block, then restore the previous values."""
+        old = {k: self.get_option(k) for k in kw}
+        try:
+            for k, v in kw.items():
+                self.set_option(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_option(k, v)
 
     def __repr__(self):
         return f"Projector(m={self.m}, p={self.p}, nnz={self.nnz}, layout={self.layout}, device={self.device})"

@@ -1,4 +1,4 @@
-"""Probe: librp dense MFMA GEMM tile variants (RP_DENSE_VARIANT) — correctness on a ragged shape
+"""Probe: librp dense MFMA GEMM tile variants (rp_dense_set_variant) — correctness on a ragged shape
 against an fp64 product, then TFLOP/s on the configs[4] block (131072 x 16384 -> 1024)."""
 import json
 import os
@@ -8,6 +8,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from randomprojection_amd import _native as nat  # noqa: E402
 from randomprojection_amd.gaussian import dense_project_device  # noqa: E402
 
 variants = [int(v) for v in sys.argv[1].split(",")]
@@ -25,7 +26,7 @@ for comp in ("bf16", "fp32"):
     out = torch.empty(131072, 1024, device="cuda")
     ref = Xs.to(dt).double().cpu().numpy() @ Cs.to(dt).double().cpu().numpy().T
     for v in variants:
-        os.environ["RP_DENSE_VARIANT"] = str(v)
+        nat.check(nat.load().rp_dense_set_variant(v))
         Y = dense_project_device(Xs, Cs, compute=comp).cpu().numpy()
         rel = float(np.linalg.norm(Y - ref) / np.linalg.norm(ref))
         for _ in range(2):

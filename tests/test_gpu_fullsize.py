@@ -86,10 +86,10 @@ def test_configs1_full_size(kdd, dist, monkeypatch):
             # the device's choice: staged gathers for uniform columns (each gather a fresh line),
             # direct for power-law ones (hot features stay in L2)
             assert project.staged == (dist == "uniform")
-            monkeypatch.setenv("RP_PIPE", "tile")
+            P.set_option("pipeline", "tile")
             P.set_staging("off")
             Tp, Tj, Tx, tn = project(P, Ap, Aj, Ax, order=order)
-            monkeypatch.delenv("RP_PIPE")
+            P.set_option("pipeline", None)
             P.set_staging("auto")
             assert tn == nnz and bool(torch.equal(Tp, Cp))
             for s in range(0, nnz, 1 << 28):

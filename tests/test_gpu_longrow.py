@@ -51,10 +51,11 @@ def test_longrow_small_p_collisions():
 
 
 @pytest.mark.parametrize("polls", ["0", "-1"])
-def test_longrow_deferral(polls, monkeypatch):
+def test_longrow_deferral(polls):
     rng = np.random.default_rng(9)
     m, p = 2_000_000, 1024
     R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
     A = kdd_like(rng, 20_000, m, mean=99, powerlaw=True, values="normal")
-    monkeypatch.setenv("RP_DEFER_POLLS", polls)
-    _check(Projector(R), A, R)
+    P = Projector(R)
+    P.set_option("defer_polls", int(polls))
+    _check(P, A, R)

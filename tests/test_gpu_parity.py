@@ -260,10 +260,9 @@ def test_index64_inputs_follow_scipy_dtype_rule():
 
 
 @pytest.mark.parametrize("threads", ["4", "0"])
-def test_large_host_fetch_pipelined(threads, monkeypatch):
+def test_large_host_fetch_pipelined(threads):
     """Outputs past 16 MB are downloaded in chunks while helper threads pre-fault the fresh numpy
-    destinations (RP_HOST_THREADS=0: plain copies); every index/value dtype combination."""
-    monkeypatch.setenv("RP_HOST_THREADS", threads)  # 4 = the default
+    destinations (option host_threads=0: plain copies); every index/value dtype combination."""
     rng = np.random.default_rng(21)
     m, p, n = 2_000_000, 4096, 1_500_000
     R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
@@ -275,6 +274,7 @@ def test_large_host_fetch_pipelined(threads, monkeypatch):
     Cp, Cj, Cx = oracle_product(A, R)
     assert Cj.size * 8 > (16 << 20)
     P = Projector(R)
+    P.set_option("host_threads", int(threads))  # 4 = the default
     for dt in (np.int32, np.int64):
         ip, ix, dx = P.project_arrays(A.indptr, A.indices, A.data, out_index_dtype=dt)
         assert ip.dtype == ix.dtype == dt

@@ -128,16 +128,16 @@ def test_staging_arguments():
 
 @pytest.mark.parametrize("polls", ["0", "-1", "3"])
 @pytest.mark.parametrize("staged", [False, True])
-def test_deferred_output_tiles(R2m, polls, staged, monkeypatch):
-    """Tiles that park their output (RP_DEFER_POLLS=0: nearly all) and tiles that wait (-1) give
-    the same bits; mixed with heavy tiles, empty rows, both orders."""
-    monkeypatch.setenv("RP_DEFER_POLLS", polls)
+def test_deferred_output_tiles(R2m, polls, staged):
+    """Tiles that park their output (option defer_polls=0: nearly all) and tiles that wait (-1)
+    give the same bits; mixed with heavy tiles, empty rows, both orders."""
     rng = np.random.default_rng(31)
     m = R2m.shape[0]
     A = sp.vstack([kdd_like(rng, 20_000, m, values="normal"), sp.csr_matrix((300, m), dtype=np.float32),
                    kdd_like(rng, 40, m, mean=300, values="normal"),
                    kdd_like(rng, 20_000, m, powerlaw=True, values="normal")]).tocsr()
     P = _staged(R2m, 16) if staged else Projector(R2m)
+    P.set_option("defer_polls", int(polls))
     want = oracle_product(A, R2m)
     assert_same_csr(P.matmul(A), *want)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
@@ -145,24 +145,24 @@ def test_deferred_output_tiles(R2m, polls, staged, monkeypatch):
 
 
 @pytest.mark.parametrize("ticks", ["1", "300", "100000"])
-def test_deferred_output_time_budget(R2m, ticks, monkeypatch):
-    """256-row tiles wait up to RP_DEFER_TICKS s_memrealtime ticks (default 800 = 8 us) before
+def test_deferred_output_time_budget(R2m, ticks):
+    """256-row tiles wait up to defer_ticks s_memrealtime ticks (default 800 = 8 us) before
     parking their output: every budget gives the oracle's bits."""
-    monkeypatch.setenv("RP_DEFER_TICKS", ticks)
     rng = np.random.default_rng(57)
     m = R2m.shape[0]
     A = sp.vstack([kdd_like(rng, 25_000, m, values="normal"), sp.csr_matrix((200, m), dtype=np.float32),
                    kdd_like(rng, 25_000, m, powerlaw=True, values="normal")]).tocsr()
     want = oracle_product(A, R2m)
-    assert_same_csr(Projector(R2m).matmul(A), *want)
+    P = Projector(R2m)
+    P.set_option("defer_ticks", int(ticks))
+    assert_same_csr(P.matmul(A), *want)
 
 
 @pytest.mark.parametrize("pipe", ["tile", "lpr"])
-def test_pipelines_multi_group_vs_oracle(R2m_p1k, pipe, monkeypatch):
-    """Each pipeline forced (RP_PIPE), direct and staged, over 600k rows: 2344 row-lane tiles, so
+def test_pipelines_multi_group_vs_oracle(R2m_p1k, pipe):
+    """Each pipeline forced (option pipeline), direct and staged, over 600k rows: 2344 row-lane tiles, so
     the staged gather spans three 1024-tile groups and ends in a partial one; uniform and
     power-law rows, empty rows, both orders."""
-    monkeypatch.setenv("RP_PIPE", pipe)
     rng = np.random.default_rng(77)
     R = R2m_p1k
     m = R.shape[0]
@@ -172,6 +172,7 @@ def test_pipelines_multi_group_vs_oracle(R2m_p1k, pipe, monkeypatch):
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     for stage in ("off", "on"):
         P = Projector(R)
+        P.set_option("pipeline", "rowlane" if pipe == "lpr" else "tile")
         P.set_staging(stage, 19)
         assert P.plan(A.shape[0], A.nnz)["pipeline"] == ("rowlane" if pipe == "lpr" else "tile")
         assert_same_csr(P.matmul(A), *want)
@@ -180,13 +181,11 @@ def test_pipelines_multi_group_vs_oracle(R2m_p1k, pipe, monkeypatch):
 
 
 @pytest.mark.parametrize("chunk", ["256", "50000"])
-def test_rowlane_chunked_launch_vs_oracle(R2m_p1k, chunk, monkeypatch):
-    """The row-lane pipeline over several row chunks (RP_LPR_CHUNK_ROWS; huge launches such as
+def test_rowlane_chunked_launch_vs_oracle(R2m_p1k, chunk):
+    """The row-lane pipeline over several row chunks (option chunk_rows; huge launches such as
     configs[2]'s 1.08B rows run in chunks of 2^27): every chunk writes its indptr slice and its
     entries at the running total of the chunks before it. Ragged last chunk, empty rows at a chunk
     boundary, heavy rows, direct and staged, both orders, int64 output indptr."""
-    monkeypatch.setenv("RP_PIPE", "lpr")
-    monkeypatch.setenv("RP_LPR_CHUNK_ROWS", chunk)
     rng = np.random.default_rng(91)
     R = R2m_p1k
     m = R.shape[0]
@@ -198,6 +197,8 @@ def test_rowlane_chunked_launch_vs_oracle(R2m_p1k, chunk, monkeypatch):
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     for stage in ("off", "on"):
         P = Projector(R)
+        P.set_option("pipeline", "rowlane")
+        P.set_option("chunk_rows", int(chunk))
         P.set_staging(stage, 19)
         assert P.plan(A.shape[0], A.nnz) == {"pipeline": "rowlane", "staged": stage == "on",
                                              "bucket_shift": 19 if stage == "on" else 0}
@@ -228,11 +229,10 @@ def _device_int64_indptr_vs_oracle(R, A, want):
     P.close()
 
 
-def test_rowlane_staged_tile_past_one_round(R2m_p1k, monkeypatch):
+def test_rowlane_staged_tile_past_one_round(R2m_p1k):
     """A tile of 3088 entries (> 12 x 256 = one round of the staged descriptor fetch, <= the entry
     cap): the second round runs with 16 of 256 lanes in range. Regression: the run lookup shuffled
     from lanes that had left the loop (found on 500M-row runs: one tile in ~1M)."""
-    monkeypatch.setenv("RP_PIPE", "lpr")
     rng = np.random.default_rng(3088)
     R = R2m_p1k
     m = R.shape[0]
@@ -246,6 +246,7 @@ def test_rowlane_staged_tile_past_one_round(R2m_p1k, monkeypatch):
     want = oracle_product(A, R)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     P = Projector(R)
+    P.set_option("pipeline", "rowlane")
     P.set_staging("on", 16)
     assert P.plan(A.shape[0], A.nnz)["staged"]
     assert_same_csr(P.matmul(A), *want)
@@ -277,8 +278,8 @@ def test_auto_staging_choice_on_device(dist):
         Cj = torch.empty(cap, dtype=torch.int32, device="cuda")
         Cx = torch.empty(cap, dtype=torch.float32, device="cuda")
         k = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, workspace=ws, nnz_a=nnz_a)
-        if mode == "auto":
-            assert P.choice(n, nnz_a, ws) == (dist == "uniform")
+        # what ran is recorded in the workspace by every call, forced modes included
+        assert P.choice(n, nnz_a, ws) == {"auto": dist == "uniform", "on": True, "off": False}[mode]
         outs[mode] = (Cp.cpu().numpy(), Cj[:k].cpu().numpy(), Cx[:k].cpu().numpy())
         P.close()
     A = sp.csr_matrix((Ax.cpu().numpy(), Aj.cpu().numpy(), Ap.cpu().numpy()), shape=(n, m))
