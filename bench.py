@@ -113,15 +113,20 @@ def main():
     ap.add_argument("--cpu-part-rows", type=int, default=100_000,
                     help="rows per recipe partition (one per core) in the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--boundary", choices=["device", "host"], default="device",
+    ap.add_argument("--boundary", choices=["device", "host", "libsvm"], default="device",
                     help="device: inputs/outputs resident in HBM (the default line); host: host CSR in -> host "
-                         "CSR out through the chunked stream path (rp_project_stream, PCIe-inclusive)")
+                         "CSR out through the chunked stream path (rp_project_stream, PCIe-inclusive); libsvm: "
+                         "libsvm text in host memory -> GPU parse + projection -> host CSR "
+                         "(rp_libsvm_project_stream; default 20M rows)")
+    ap.add_argument("--chunk-bytes", type=int, default=64 << 20, help="--boundary libsvm: text bytes per chunk")
     ap.add_argument("--host-mem", choices=["pageable", "pinned"], default="pinned",
                     help="--boundary host: host arrays in pageable (numpy) or page-locked (rp_host_alloc) memory")
     ap.add_argument("--chunk-rows", type=int, default=0, help="--boundary host: rows per chunk (0 = library default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    if args.boundary == "libsvm" and args.rows is None:
+        args.rows = 20_000_000  # ~5 GB of text in host memory per rank
     for k in ("rows", "m", "p", "dist", "cpu_sample_rows"):
         if getattr(args, k) is None:
             setattr(args, k, cfg[k])
@@ -197,17 +202,18 @@ def main():
     nnz_a = int(Aj.numel())
     log(f"[rank {rank}] A: {args.rows} rows, nnz={nnz_a} ({time.perf_counter() - t0:.1f}s)")
 
-    if args.boundary == "host":
+    if args.boundary in ("host", "libsvm"):
+        (bench_host if args.boundary == "host" else bench_libsvm)(args, cfg, P, R_host, Ap, Aj, Ax, world, rank, dev)
         if world > 1:
-            raise SystemExit("--boundary host is a one-GPU line (each rank would stream its own shard)")
-        return bench_host(args, cfg, P, R_host, Ap, Aj, Ax)
+            dist.destroy_process_group()
+        return
 
     # ---- output buffers sized by an exact first run
     stream = torch.cuda.current_stream(dev).cuda_stream
     if args.staging != "auto" or args.stage_shift:
         P.set_staging(args.staging, args.stage_shift)
     try:  # full workspace (deferred tile output + staging); the minimal one if HBM is short
-        ws = torch.empty(P.workspace_bytes(args.rows, nnz_a), dtype=torch.uint8, device=dev)
+        ws = torch.empty(P.workspace_bytes(args.rows, nnz_a, dtype=Ax.dtype), dtype=torch.uint8, device=dev)
     except torch.OutOfMemoryError:
         log(f"[rank {rank}] full workspace does not fit: blocking look-back only")
         ws = torch.empty(P.workspace_bytes(args.rows), dtype=torch.uint8, device=dev)
@@ -368,12 +374,40 @@ class HostArrays:
         self.keep = []
 
 
-def bench_host(args, cfg, P, R_host, Ap, Aj, Ax):
+def _allreduce(x: float, op: str, dev) -> float:
+    """max/min of one float over the ranks (gloo rehearsals reduce on the CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return x
+    on = dev if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
+    return float(t.item())
+
+
+def _barrier(dev):
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.synchronize(dev)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.barrier()
+
+
+def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
     """Boundary 2: host CSR in -> host CSR out, PCIe-inclusive, through
     rp_project_stream (chunk k+1 uploading while chunk k projects and chunk k-1 downloads). The
-    timed region starts with A in host memory and ends with C in host memory."""
+    timed region starts with A in host memory and ends with C in host memory. At N ranks every rank
+    streams its OWN shard (the recipe's executors, code/clustermode/randomProjection.py:107-113)
+    from host memory on its GPU's NUMA node; no collective runs in the loop: a barrier brackets the
+    timed steps and the wall time is the max over ranks."""
     import torch
 
+    from randomprojection_amd import hostmem
+
+    numa = hostmem.bind_to_device_numa(P.device)  # before the host buffers are allocated and touched
     hm = HostArrays(args.host_mem == "pinned")
     n, nnz_a = args.rows, int(Aj.numel())
     ap = hm.empty(n + 1, np.int32 if nnz_a < 2**31 else np.int64)
@@ -393,19 +427,22 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax):
 
     for _ in range(max(args.warmup, 1)):
         cp, cj, cx = step()
+    _barrier(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         cp, cj, cx = step()
-    dt = (time.perf_counter() - t0) / args.steps
+    t_wall = time.perf_counter() - t0
+    _barrier(dev)
+    dt = _allreduce(t_wall, "max", dev) / args.steps
     nnz_c = int(cj.size)
     h2d = ap.nbytes + aj.nbytes + ax.nbytes
     d2h = cp.nbytes + cj.nbytes + cx.nbytes
-    # after the clock: a seeded sample of rows against the oracle, bit for bit
+    # after the clock: a seeded sample of this rank's rows against the oracle, bit for bit
     import scipy.sparse as sp
 
     from oracle import smmp
 
-    rng = np.random.default_rng(20261016)
+    rng = np.random.default_rng(20261016 + rank)
     rows = np.sort(rng.choice(n, size=min(4096, n), replace=False))
     A = sp.csr_matrix((ax, aj, ap), shape=(n, args.m))[rows]
     Wp, Wj, Wx, _, _ = smmp.matmat(A, R_host)
@@ -414,28 +451,128 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax):
     C = sp.csr_matrix((cx, cj, cp), shape=(n, args.p))[rows]
     same = (np.array_equal(C.indptr, Wp) and np.array_equal(C.indices, Wj)
             and np.array_equal(C.data.view(np.uint32), Wx.view(np.uint32)))
-    out_line = {
-        "metric": "rows/sec projected, host CSR in -> host CSR out (PCIe-inclusive, chunked row streaming), "
-                  "KDD2012 54.7M->4096 dims",
-        "value": n / dt, "unit": "rows/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f32", "data": cfg["data"].format(dist=args.dist, p=args.p),
-        "config": {"workload": "configs[1] host boundary: " + cfg["workload"].format(rows=n, m=args.m, p=args.p)
-                               .replace("device-resident CSR in/out", "host CSR in/out"),
-                   "boundary": "host", "host_mem": args.host_mem, "chunk_rows": args.chunk_rows or 2 << 20,
-                   "nnz_in": nnz_a, "nnz_out": nnz_c, "order": order},
-        "pcie": {"h2d_bytes": h2d, "d2h_bytes": d2h, "h2d_GBps": h2d / dt / 1e9, "d2h_GBps": d2h / dt / 1e9,
-                 "link_peak_GBps_per_direction": 63.0, "measured_copy_GBps": "H2D ~55, D2H 48-55 concurrently "
-                 "(scripts/probes/pcie_probe2.hip)"},
-        "roofline": {"bound": "pcie", "achieved": h2d / dt / 1e9, "peak": 63.0, "unit": "GB/s",
-                     "frac": h2d / dt / 1e9 / 63.0, "traffic": None,
-                     "note": "the upload direction binds (92 B/row in vs 53 B/row out); kernel roofline: the "
-                             "device-resident line"},
-        "cpu_baseline": None,
-        "verified": {"sample_rows": int(rows.size), "sample_bitexact_vs_oracle": bool(same),
-                     "indptr_ok": bool(cp[0] == 0 and int(cp[-1]) == nnz_c)},
-    }
-    print(json.dumps(out_line), flush=True)
+    same_all = _allreduce(1.0 if same else 0.0, "min", dev) == 1.0
+    ptr_ok = _allreduce(1.0 if (cp[0] == 0 and int(cp[-1]) == nnz_c) else 0.0, "min", dev) == 1.0
+    nnz_all = _allreduce(float(nnz_c), "max", dev)
+    if rank == 0:
+        out_line = {
+            "metric": "rows/sec projected (whole node), host CSR in -> host CSR out (PCIe-inclusive, chunked row "
+                      "streaming), KDD2012 54.7M->4096 dims",
+            "value": n * world / dt, "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": cfg["data"].format(dist=args.dist, p=args.p),
+            "config": {"workload": "configs[1] host boundary: " + cfg["workload"].format(rows=n, m=args.m, p=args.p)
+                                   .replace("device-resident CSR in/out", "host CSR in/out"),
+                       "boundary": "host", "host_mem": args.host_mem, "chunk_rows": args.chunk_rows or 2 << 20,
+                       "rows_per_gpu": n, "nnz_in": nnz_a, "nnz_out": nnz_c, "max_nnz_out_over_ranks": int(nnz_all),
+                       "order": order, "parallelism": f"row-shard x{world}, own shard per rank, no collective in the loop",
+                       "numa_rank0": numa},
+            "pcie": {"h2d_bytes_per_gpu": h2d, "d2h_bytes_per_gpu": d2h, "h2d_GBps_per_gpu": h2d / dt / 1e9,
+                     "d2h_GBps_per_gpu": d2h / dt / 1e9, "host_dram_GBps_node": (h2d + d2h) * world / dt / 1e9,
+                     "link_peak_GBps_per_direction": 63.0, "measured_copy_GBps": "H2D ~55, D2H 48-55 concurrently "
+                     "(scripts/probes/pcie_probe2.hip)"},
+            "roofline": {"bound": "pcie", "achieved": h2d / dt / 1e9, "peak": 63.0, "unit": "GB/s",
+                         "frac": h2d / dt / 1e9 / 63.0, "traffic": None,
+                         "note": "per GPU: the upload direction binds (92 B/row in vs 53 B/row out); kernel "
+                                 "roofline: the device-resident line"},
+            "cpu_baseline": None,
+            "verified": {"sample_rows_per_rank": int(rows.size), "sample_bitexact_vs_oracle": bool(same_all),
+                         "indptr_ok": bool(ptr_ok)},
+        }
+        print(json.dumps(out_line), flush=True)
+    hm.free()
+
+
+def bench_libsvm(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
+    """Boundary 3: libsvm text in host memory -> GPU parse -> projection -> host
+    CSR, through rp_libsvm_project_stream (chunks of whole lines: chunk k+1 uploading while chunk k
+    is parsed and projected and chunk k-1 downloads). Replaces spark.read.format("libsvm") + the
+    partition function's product (code/clustermode/randomProjection.py:71-72, :46). The text is
+    configs[1]-shaped rows written by rp_synth_libsvm_device (values of 6-17 significant digits),
+    copied to page-locked host memory before the clock; the timed region starts with the text in
+    host memory and ends with labels + CSR in host memory. At N ranks every rank streams its own
+    text; no collective in the loop."""
+    import ctypes
+
+    import torch
+
+    from randomprojection_amd import hostmem, libsvm, synth
+
+    numa = hostmem.bind_to_device_numa(P.device)
+    n = args.rows
+    text_d, off_d = synth.libsvm_text_device(Ap, Aj, seed=11 + rank)
+    nbytes = int(text_d.numel())
+    hm = HostArrays(args.host_mem == "pinned")
+    text = hm.empty(nbytes, np.uint8)
+    torch.from_numpy(text).copy_(text_d)
+    offs = off_d.cpu().numpy()
+    nnz_a = int(Aj.numel())
+    del text_d, off_d, Ap, Aj, Ax
+    torch.cuda.empty_cache()
+    exp = nnz_a * P.nnz / P.m
+    cap = int(1.02 * exp + 8 * np.sqrt(exp)) + 65536
+    it = np.int32 if cap < 2**31 else np.int64
+    out = (hm.empty(n, np.float64), hm.empty(n + 1, it), hm.empty(cap, np.int32), hm.empty(cap, np.float32))
+    order = args.order
+
+    def step():
+        return libsvm.project_text_stream(text, P, order=order, chunk_bytes=args.chunk_bytes, out=out)
+
+    for _ in range(max(args.warmup, 1)):
+        lab, cp, cj, cx = step()
+    _barrier(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lab, cp, cj, cx = step()
+    t_wall = time.perf_counter() - t0
+    _barrier(dev)
+    dt = _allreduce(t_wall, "max", dev) / args.steps
+    nnz_c = int(cj.size)
+    # after the clock: a seeded sample of lines parsed by the oracle (Spark's parseLibSVMRecord
+    # restated, oracle/libsvm_ref.py) and projected by the scipy-kernel restatement, bit for bit
+    import scipy.sparse as sp
+
+    from oracle import smmp
+    from oracle.libsvm_ref import parse_text
+
+    rng = np.random.default_rng(20261017 + rank)
+    rows = np.sort(rng.choice(n, size=min(2048, n), replace=False))
+    sample = b"".join(text[offs[r]:offs[r + 1]].tobytes() for r in rows)
+    l_ref, p_ref, j_ref, v_ref = parse_text(sample, args.m)
+    A = sp.csr_matrix((v_ref, j_ref, p_ref), shape=(rows.size, args.m))
+    Wp, Wj, Wx, _, _ = smmp.matmat(A, R_host)
+    if order == "sorted":
+        Wj, Wx = smmp.sorted_rows(Wp, Wj, Wx)
+    C = sp.csr_matrix((cx, cj, cp), shape=(n, args.p))[rows]
+    same = (int(lab.size) == n and np.array_equal(lab[rows], l_ref) and np.array_equal(C.indptr, Wp)
+            and np.array_equal(C.indices, Wj) and np.array_equal(C.data.view(np.uint32), Wx.view(np.uint32)))
+    same_all = _allreduce(1.0 if same else 0.0, "min", dev) == 1.0
+    d2h = lab.nbytes + cp.nbytes + cj.nbytes + cx.nbytes
+    if rank == 0:
+        line = {
+            "metric": "rows/sec projected (whole node), libsvm text in host memory -> GPU parse + projection -> "
+                      "host CSR (PCIe-inclusive, chunked), KDD2012 54.7M->4096 dims",
+            "value": n * world / dt, "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic configs[1]-shaped libsvm text (uniform columns, 1+Poisson(10) items per line, values "
+                    "with 6-17 significant digits, labels 0/1; rp_synth_libsvm_device), R = "
+                    f"SparseRandomProjection({args.p}, random_state=123)",
+            "config": {"workload": f"boundary 3: {n} libsvm lines per GPU x {args.m} -> {args.p}, text in "
+                                   f"{args.host_mem} host memory, {args.chunk_bytes >> 20} MB chunks",
+                       "boundary": "libsvm", "rows_per_gpu": n, "text_bytes_per_gpu": nbytes,
+                       "bytes_per_line": nbytes / n, "nnz_in": nnz_a, "nnz_out": nnz_c, "order": order,
+                       "parallelism": f"own text per rank x{world}, no collective in the loop", "numa_rank0": numa},
+            "text_GBps_per_gpu": nbytes / dt / 1e9,
+            "roofline": {"bound": "pcie", "achieved": (nbytes + d2h) / dt / 1e9, "peak": 2 * 63.0, "unit": "GB/s",
+                         "frac": (nbytes + d2h) / dt / 1e9 / 126.0, "traffic": None,
+                         "h2d_GBps": nbytes / dt / 1e9, "d2h_GBps": d2h / dt / 1e9,
+                         "note": "PCIe Gen5 x16 both directions (63 GB/s each); text up, labels + CSR down"},
+            "cpu_baseline": None,
+            "verified": {"sample_lines_per_rank": int(rows.size), "sample_bitexact_vs_oracle": bool(same_all),
+                         "oracle": "oracle/libsvm_ref.py (Spark parseLibSVMRecord + Java double) + oracle/smmp.c"},
+        }
+        print(json.dumps(line), flush=True)
     hm.free()
 
 

@@ -150,6 +150,9 @@ int rp_pack_r_host(int64_t m, int64_t p, const void* indptr, int32_t indptr_type
  * states + counters, plus the staged-gather buffers (about 8 bytes per A entry) when the launch
  * would stage. nnz_a < 0 (unknown): the small look-back part for the worst-case tiling only. */
 int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_t nnz_a);
+/* The same for a known compute type (RP_F32 / RP_F64): the value-sized parts (deferred-output pool,
+ * row-lane slots) sized for it rather than for float64 (configs[3] at 200M rows: 40 GB, not 66). */
+int64_t rp_project_workspace_bytes_for(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t data_type);
 
 /* Staged gather (packed R, m < 2^30): the A entries of each tile are bucketed by feature range and
  * R's descriptors fetched bucket by bucket from an L2-resident slice (three launches instead of one
@@ -263,6 +266,28 @@ int rp_libsvm_parse_device(int device, const char* text, int64_t n_bytes, int64_
                            double* labels, void* indptr, int32_t indptr_type, int32_t* indices,
                            float* data, int64_t cap_rows, int64_t cap_nnz, void* stream,
                            int64_t* n_rows, int64_t* nnz, int64_t* err_line);
+
+/* Boundary 3, chunked: libsvm text in host memory -> GPU parse -> projection -> host CSR.
+ * Replaces spark.read.format("libsvm").load(...) followed by the partition function's projection
+ * (code/clustermode/randomProjection.py:71-72 then :46 inside mapPartitions, :107-110). The text is
+ * cut into chunks of whole lines of about chunk_bytes (0 = 64 MB, a Spark text partition); chunk
+ * k+1's upload, chunk k's parse + projection and chunk k-1's download overlap (an upload thread, a
+ * compute stream, a download thread). Parsing follows rp_libsvm_parse_device (float32 values, so R
+ * must be float32: the recipe's astype). Outputs: labels[cap_rows] (f64), c_host = the projected CSR
+ * (indptr cap_rows + 1 entries, indices/data capacity entries, data float32), *n_rows, *total_nnz.
+ * RP_ERR_CAPACITY when rows exceed cap_rows or entries exceed capacity (then *n_rows / *total_nnz
+ * report what was needed as far as known); RP_ERR_INVALID with *err_line = 0-based line of the file
+ * for a malformed line. Host arrays may be pinned (rp_host_alloc) or pageable. */
+int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes, int32_t order, int64_t chunk_bytes,
+                             double* labels, int64_t cap_rows, const rp_csr_out* c_host, int64_t* n_rows,
+                             int64_t* total_nnz, int64_t* err_line);
+
+/* Synthetic libsvm text on the device (benchmarks of boundary 3): row i of a device CSR (int64
+ * indptr, int32 indices) as "<0|1> <j+1>:<value> ..." with decimal values of 6-17 significant
+ * digits. line_offsets: device int64[n_rows + 1], filled with each line's start (and the total).
+ * With text == NULL only *n_bytes is computed; then text (cap_bytes, device) is written. */
+int rp_synth_libsvm_device(int device, int64_t n_rows, const int64_t* indptr, const int32_t* indices, uint64_t seed,
+                           int64_t* line_offsets, char* text, int64_t cap_bytes, void* stream, int64_t* n_bytes);
 
 /* Dense Gaussian projection (BASELINE configs[4]): Y[n x p] (f32, row stride ldy) = X[n x m] .
  * G[p x m]^T for device arrays X and G of dtype RP_F32 (exact-f32 MFMA products, f32 accumulate) or

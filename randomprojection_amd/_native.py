@@ -23,10 +23,10 @@ EXPORTS = (
     "rp_last_error", "rp_version", "rp_device_count",
     "rp_projector_create", "rp_projector_info_get", "rp_projector_export",
     "rp_projector_create_from_device", "rp_projector_destroy", "rp_pack_r_host",
-    "rp_project_workspace_bytes", "rp_project_plan", "rp_project_choice", "rp_projector_set_staging",
+    "rp_project_workspace_bytes", "rp_project_workspace_bytes_for", "rp_project_plan", "rp_project_choice", "rp_projector_set_staging",
     "rp_projector_set_option", "rp_projector_get_option", "rp_project_device",
     "rp_project_host_begin", "rp_result_fetch", "rp_result_free", "rp_project",
-    "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_project_stream", "rp_host_alloc", "rp_host_free",
+    "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_libsvm_project_stream", "rp_synth_libsvm_device", "rp_project_stream", "rp_host_alloc", "rp_host_free",
     "rp_dense_project_device", "rp_dense_set_variant",
 )
 
@@ -109,6 +109,7 @@ def load(path: str = None):
         "rp_projector_destroy": (ctypes.c_int, [vp]),
         "rp_pack_r_host": (ctypes.c_int, [i64, i64, vp, i32, vp, i32, vp, i32, i32, P(ProjectorInfo), vp, vp, vp]),
         "rp_project_workspace_bytes": (i64, [vp, i64, i64]),
+        "rp_project_workspace_bytes_for": (i64, [vp, i64, i64, i32]),
         "rp_project_plan": (ctypes.c_int, [vp, i64, i64, P(i32), P(i32), P(i32)]),
         "rp_project_choice": (ctypes.c_int, [vp, i64, i64, vp, P(i32)]),
         "rp_projector_set_staging": (ctypes.c_int, [vp, i32, i32]),
@@ -128,6 +129,10 @@ def load(path: str = None):
         "rp_dense_set_variant": (ctypes.c_int, [i32]),
         "rp_libsvm_parse_device": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, vp, vp, i32, vp, vp, i64, i64, vp,
                                                   P(i64), P(i64), P(i64)]),
+        "rp_libsvm_project_stream": (ctypes.c_int, [vp, vp, i64, i32, i64, vp, i64, P(CsrOut), P(i64), P(i64),
+                                                    P(i64)]),
+        "rp_synth_libsvm_device": (ctypes.c_int, [ctypes.c_int, i64, vp, vp, ctypes.c_uint64, vp, vp, i64, vp,
+                                                  P(i64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name, None)

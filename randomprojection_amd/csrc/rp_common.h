@@ -90,4 +90,14 @@ inline double val_at(const void* a, int t, int64_t i) {
 // inclusive prefix sum of n int64 values in place on `st` (defined in rp_spgemm.hip)
 int inclusive_scan_i64(int64_t* a, int64_t n, hipStream_t st, DevBuf& tmp, int device);
 
+// libsvm parse (rp_libsvm.hip) with caller-kept scratch buffers, so a chunked pipeline allocates
+// once (hipFree of a per-call buffer would synchronise the device and stall the other streams).
+// Same contract as rp_libsvm_parse_device, on stream st.
+struct LibsvmScratch {
+    DevBuf counts, tmp, nl, keep, items, errb, slow;
+};
+int libsvm_parse(LibsvmScratch& s, int device, const char* text, int64_t n_bytes, int64_t num_features,
+                 double* labels, void* indptr, int32_t indptr_type, int32_t* indices, float* data, int64_t cap_rows,
+                 int64_t cap_nnz, hipStream_t st, int64_t* n_rows, int64_t* nnz, int64_t* err_line);
+
 }  // namespace rpd

@@ -615,19 +615,19 @@ const char* reason(int c) {
 
 }  // namespace
 
-extern "C" int rp_libsvm_parse_device(int device, const char* text, int64_t n_bytes, int64_t num_features,
-                                      double* labels, void* indptr, int32_t indptr_type, int32_t* indices,
-                                      float* data, int64_t cap_rows, int64_t cap_nnz, void* stream,
-                                      int64_t* n_rows, int64_t* nnz, int64_t* err_line) {
+int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n_bytes, int64_t num_features,
+                      double* labels, void* indptr, int32_t indptr_type, int32_t* indices, float* data,
+                      int64_t cap_rows, int64_t cap_nnz, hipStream_t st, int64_t* n_rows, int64_t* nnz,
+                      int64_t* err_line) {
     if (!n_rows || !nnz || n_bytes < 0 || (n_bytes > 0 && !text)) return fail(RP_ERR_INVALID, "bad argument");
     if (indptr && indptr_type != RP_I32 && indptr_type != RP_I64) return fail(RP_ERR_INVALID, "bad indptr type");
     if (err_line) *err_line = -1;
     HIP_TRY(hipSetDevice(device));
-    hipStream_t st = (hipStream_t)stream;
     const unsigned char* t = (const unsigned char*)text;
     if (((uintptr_t)t & 15) != 0) return fail(RP_ERR_INVALID, "text must be 16-byte aligned");
     const int64_t nblk = std::max<int64_t>((n_bytes + kBytesPerBlock - 1) / kBytesPerBlock, 1);
-    DevBuf counts, tmp, nl, keep, items, errb, slow;
+    DevBuf &counts = sc.counts, &tmp = sc.tmp, &nl = sc.nl, &keep = sc.keep, &items = sc.items, &errb = sc.errb,
+           &slow = sc.slow;
     int rc;
     if ((rc = counts.ensure(8 * (size_t)nblk, device))) return rc;
     hipLaunchKernelGGL(nl_count_kernel, dim3((unsigned)nblk), dim3(kLB), 0, st, t, n_bytes, (int64_t*)counts.p);
@@ -712,5 +712,119 @@ extern "C" int rp_libsvm_parse_device(int device, const char* text, int64_t n_by
         if (err_line) *err_line = (int64_t)(e >> 8);
         return fail(RP_ERR_INVALID, "libsvm line %lld: %s", (long long)(e >> 8), reason((int)(e & 0xff)));
     }
+    return RP_OK;
+}
+
+extern "C" int rp_libsvm_parse_device(int device, const char* text, int64_t n_bytes, int64_t num_features,
+                                      double* labels, void* indptr, int32_t indptr_type, int32_t* indices,
+                                      float* data, int64_t cap_rows, int64_t cap_nnz, void* stream,
+                                      int64_t* n_rows, int64_t* nnz, int64_t* err_line) {
+    LibsvmScratch sc;
+    return libsvm_parse(sc, device, text, n_bytes, num_features, labels, indptr, indptr_type, indices, data,
+                        cap_rows, cap_nnz, (hipStream_t)stream, n_rows, nnz, err_line);
+}
+
+// ------------------------------------------------------------------------------------------
+// Synthetic libsvm text (benchmarks of boundary 3; the reference reads kdd12.tr, not available
+// offline): row i of a device CSR as "<label> <j+1>:<value> ...\n", label 0/1, every value a
+// decimal literal of 6-17 significant digits (first digit 1-9, a decimal point after a random
+// digit or none, a minus sign on a quarter of them) — the literal shapes that exercise both the
+// fast and the exact paths of the parser. Deterministic in (seed, entry index).
+namespace {
+__device__ __forceinline__ uint64_t sx_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ int sx_digits(uint64_t v) {
+    int d = 1;
+    while (v >= 10) {
+        v /= 10;
+        ++d;
+    }
+    return d;
+}
+struct SxValue {
+    uint64_t r;  // digit source
+    int k, q;    // significant digits, digits before the point (q == k: no point)
+    bool neg;
+    __device__ SxValue(uint64_t seed, int64_t e) {
+        const uint64_t h = sx_mix(seed ^ ((uint64_t)e * 0xD1B54A32D192ED03ull));
+        k = 6 + (int)(h % 12u);
+        q = 1 + (int)((h >> 8) % (uint64_t)k);
+        neg = ((h >> 20) & 3u) == 0;
+        r = sx_mix(h);
+    }
+    __device__ int len() const { return (neg ? 1 : 0) + k + (q < k ? 1 : 0); }
+};
+
+__global__ void sx_len_kernel(int64_t n_rows, const int64_t* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                              uint64_t seed, int64_t* __restrict__ len) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_rows; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t L = 2;  // label + newline
+        for (int64_t e = Ap[i]; e < Ap[i + 1]; ++e)
+            L += 2 + sx_digits((uint64_t)Aj[e] + 1) + SxValue(seed, e).len();
+        len[i + 1] = L;
+    }
+}
+
+__global__ void sx_write_kernel(int64_t n_rows, const int64_t* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                                uint64_t seed, const int64_t* __restrict__ off, char* __restrict__ text) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_rows; i += (int64_t)gridDim.x * blockDim.x) {
+        char* o = text + off[i];
+        *o++ = (sx_mix(seed + 0x51ED27ull * (uint64_t)i) & 1u) ? '1' : '0';
+        for (int64_t e = Ap[i]; e < Ap[i + 1]; ++e) {
+            *o++ = ' ';
+            const uint64_t j = (uint64_t)Aj[e] + 1;
+            const int dj = sx_digits(j);
+            uint64_t v = j;
+            for (int d = dj - 1; d >= 0; --d) {
+                o[d] = (char)('0' + v % 10);
+                v /= 10;
+            }
+            o += dj;
+            *o++ = ':';
+            SxValue x(seed, e);
+            if (x.neg) *o++ = '-';
+            uint64_t r = x.r;
+            for (int d = 0; d < x.k; ++d) {
+                if (d == x.q) *o++ = '.';
+                const uint32_t dig = d == 0 ? 1u + (uint32_t)(r % 9u) : (uint32_t)(r % 10u);
+                r = d % 16 == 15 ? sx_mix(r) : r / 10;
+                *o++ = (char)('0' + dig);
+            }
+        }
+        *o = '\n';
+    }
+}
+}  // namespace
+
+extern "C" int rp_synth_libsvm_device(int device, int64_t n_rows, const int64_t* indptr, const int32_t* indices,
+                                      uint64_t seed, int64_t* line_offsets, char* text, int64_t cap_bytes,
+                                      void* stream, int64_t* n_bytes) {
+    if (n_rows < 0 || !indptr || !line_offsets || !n_bytes) return fail(RP_ERR_INVALID, "bad argument");
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t st = (hipStream_t)stream;
+    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_rows + 255) / 256, 1), 65536);
+    HIP_TRY(hipMemsetAsync(line_offsets, 0, 8, st));
+    if (n_rows > 0) {
+        hipLaunchKernelGGL(sx_len_kernel, dim3(grid), dim3(256), 0, st, n_rows, indptr, indices, seed, line_offsets);
+        HIP_TRY(hipGetLastError());
+        DevBuf tmp;
+        if (int rc = inclusive_scan_i64(line_offsets + 1, n_rows, st, tmp, device)) return rc;
+    }
+    int64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, line_offsets + n_rows, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    *n_bytes = total;
+    if (!text) return RP_OK;
+    if (total > cap_bytes) return fail(RP_ERR_CAPACITY, "text needs %lld bytes", (long long)total);
+    if (n_rows > 0) {
+        hipLaunchKernelGGL(sx_write_kernel, dim3(grid), dim3(256), 0, st, n_rows, indptr, indices, seed, line_offsets,
+                           text);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipStreamSynchronize(st));
     return RP_OK;
 }

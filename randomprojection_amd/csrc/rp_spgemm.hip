@@ -3373,6 +3373,12 @@ int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_
     return (int64_t)make_plan(h, n_rows, nnz_a).total;
 }
 
+int64_t rp_project_workspace_bytes_for(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t data_type) {
+    if (data_type != RP_F32 && data_type != RP_F64) return -1;
+    if (!h || n_rows < 0 || nnz_a < 0) return rp_project_workspace_bytes(h, n_rows, nnz_a);
+    return (int64_t)make_plan(h, n_rows, nnz_a, true, dtype_size(data_type)).total;
+}
+
 int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t* pipeline, int32_t* staged,
                     int32_t* bucket_shift) {
     if (!h || n_rows < 0) return fail(RP_ERR_INVALID, "NULL projector or n_rows < 0");
@@ -3815,6 +3821,9 @@ int stream_upload(const rp_csr_in* a, const StreamChunk& ck, StreamSlot& s, hipS
     return RP_OK;
 }
 
+int stream_project(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int order, int vt, int out_ip, int out_ix,
+                   unsigned long long* total, bool last, hipStream_t st);
+
 // the chunk's kernels on the compute stream; output capacity s.cap (the exact nnz lands in info[1])
 int stream_compute(rp_projector* h, const rp_csr_in* a, const StreamChunk& ck, StreamSlot& s, int order,
                    int ip_type, int vt,
@@ -3845,6 +3854,14 @@ int stream_compute(rp_projector* h, const rp_csr_in* a, const StreamChunk& ck, S
     if (chk[2] != ~0ull)
         return fail(RP_ERR_INVALID, "A column index %d out of range [0, %lld)", a->indices[ck.e0 + (int64_t)chk[2]],
                     (long long)h->m);
+    return stream_project(h, ck, s, order, vt, out_ip, out_ix, total, last, st);
+}
+
+// the projection part of a chunk: its CSR is in s.ap (int64, from 0) / s.aj / s.ax on the device;
+// output offsets chained on the device through `total`
+int stream_project(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int order, int vt, int out_ip, int out_ix,
+                   unsigned long long* total, bool last, hipStream_t st) {
+    unsigned long long* info = (unsigned long long*)s.info.p;
     rp_csr_in ad{ck.rows, s.ap.p, RP_I64, (const int32_t*)s.aj.p, s.ax.p, vt, ck.nnz};
     rp_csr_out cd{s.cp.p, RP_I64, s.cj.p, RP_I32, s.cx.p, s.cap};
     int rc = project_device_impl(h, &ad, &cd, order, s.ws.p, (int64_t)s.ws.bytes, st, nullptr, ck.nnz);
@@ -4060,6 +4077,220 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
     (void)hipStreamSynchronize(st_comp);
     cleanup();
     if (rc) return rc;
+    if (total_nnz) *total_nnz = total;
+    if (total > c->capacity)
+        return fail(RP_ERR_CAPACITY, "output capacity %lld < nnz %lld", (long long)c->capacity, (long long)total);
+    if (c->indptr_type == RP_I32 && total > INT32_MAX)
+        return fail(RP_ERR_CAPACITY, "nnz %lld needs an int64 output indptr", (long long)total);
+    return RP_OK;
+}
+
+// Boundary 3 (libsvm text -> projected CSR), chunked like rp_project_stream: chunk k+1's text
+// uploads while chunk k is parsed and projected and chunk k-1's result downloads. A chunk is a run of
+// whole lines (a Spark text partition); its rows land at the running row total, its entries at the
+// running output total (chained on the device). Parse scratch and slot buffers grow only, so the
+// steady state allocates nothing.
+namespace {
+struct TextSlot {
+    DevBuf text, labels;
+    LibsvmScratch ps;
+    StreamSlot s;
+};
+struct TextChunk {
+    int64_t b0, bytes;
+};
+
+int64_t lines_before(const char* text, int64_t b) {  // error reporting only
+    int64_t n = 0;
+    for (const char* p = text; (p = (const char*)memchr(p, '\n', (size_t)(text + b - p))) != nullptr; ++p) ++n;
+    return n;
+}
+}  // namespace
+
+int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes, int32_t order, int64_t chunk_bytes,
+                             double* labels, int64_t cap_rows, const rp_csr_out* c, int64_t* n_rows,
+                             int64_t* total_nnz, int64_t* err_line) {
+    if (err_line) *err_line = -1;
+    if (!h || !c || !n_rows || n_bytes < 0 || (n_bytes > 0 && !text)) return fail(RP_ERR_INVALID, "bad argument");
+    if (order != RP_ORDER_SCIPY && order != RP_ORDER_SORTED) return fail(RP_ERR_INVALID, "bad order");
+    if (h->value_type != RP_F32)
+        return fail(RP_ERR_UNSUPPORTED, "libsvm values are float32 (the recipe's astype): R must be float32");
+    if ((c->indptr_type != RP_I32 && c->indptr_type != RP_I64) || (c->indices_type != RP_I32 && c->indices_type != RP_I64))
+        return fail(RP_ERR_INVALID, "bad output index types");
+    if (!c->indptr || (c->capacity > 0 && (!c->indices || !c->data)) || (cap_rows > 0 && !labels))
+        return fail(RP_ERR_INVALID, "NULL output arrays");
+    if (chunk_bytes <= 0) chunk_bytes = 64ll << 20;
+    std::vector<TextChunk> chunks;
+    for (int64_t b = 0; b < n_bytes;) {
+        int64_t e = std::min(n_bytes, b + chunk_bytes);
+        if (e < n_bytes) {  // end after the last newline inside, or after the line that spans the cut
+            const char* nl = (const char*)memrchr(text + b, '\n', (size_t)(e - b));
+            if (nl) {
+                e = nl - text + 1;
+            } else {
+                const char* nx = (const char*)memchr(text + e, '\n', (size_t)(n_bytes - e));
+                e = nx ? nx - text + 1 : n_bytes;
+            }
+        }
+        chunks.push_back({b, e - b});
+        b = e;
+    }
+    std::lock_guard<std::mutex> lock(h->mu);
+    HIP_TRY(hipSetDevice(h->device));
+    *n_rows = 0;
+    if (total_nnz) *total_nnz = 0;
+    if (chunks.empty()) {
+        if (c->indptr_type == RP_I64) ((int64_t*)c->indptr)[0] = 0; else ((int32_t*)c->indptr)[0] = 0;
+        return RP_OK;
+    }
+    const int ns = (int)std::min<size_t>(kStreamSlots, chunks.size());
+    TextSlot slots[kStreamSlots];
+    std::vector<StreamChunk> cks(chunks.size());
+    int rc;
+    for (int i = 0; i < ns; ++i) HIP_TRY(hipEventCreateWithFlags(&slots[i].s.comp, hipEventDisableTiming));
+    DevBuf totbuf;
+    hipStream_t st_up = nullptr, st_comp = nullptr, st_down = nullptr;
+    auto cleanup = [&] {
+        for (auto& t : slots)
+            if (t.s.comp) (void)hipEventDestroy(t.s.comp);
+        for (hipStream_t q : {st_up, st_comp, st_down})
+            if (q) (void)hipStreamDestroy(q);
+    };
+    if ((rc = totbuf.ensure(8, h->device))) {
+        cleanup();
+        return rc;
+    }
+    if (hipStreamCreateWithFlags(&st_up, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&st_comp, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&st_down, hipStreamNonBlocking) != hipSuccess ||
+        hipMemsetAsync(totbuf.p, 0, 8, st_comp) != hipSuccess) {
+        cleanup();
+        return fail(RP_ERR_HIP, "stream setup failed");
+    }
+    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
+    auto out_cap = [&](int64_t nnz) {
+        const double ex = ppe * (double)nnz;
+        return (int64_t)(1.05 * ex + 8.0 * std::sqrt(ex + 1.0)) + 4096;
+    };
+    const int dev = h->device;
+    const int64_t K = (int64_t)chunks.size();
+    StreamSync sy;
+    std::vector<int64_t> knnz((size_t)K, 0);
+    std::vector<char> redo((size_t)K, 0);
+    int64_t bad_line = -1;
+    auto upload = [&](int64_t k, TextSlot& t) -> int {
+        const TextChunk& tc = chunks[(size_t)k];
+        if (int r = t.text.ensure((size_t)tc.bytes + 16, dev)) return r;
+        HIP_TRY(hipMemcpyAsync(t.text.p, text + tc.b0, (size_t)tc.bytes, hipMemcpyHostToDevice, st_up));
+        HIP_TRY(hipStreamSynchronize(st_up));
+        return RP_OK;
+    };
+    // parse chunk k in slot t (on st_comp) into t.s.ap/aj/ax and t.labels; fills cks[k] but r0
+    auto parse = [&](int64_t k, TextSlot& t, int64_t cap_out) -> int {
+        const TextChunk& tc = chunks[(size_t)k];
+        int64_t rows = 0, nnz = 0, el = -1;
+        int r = libsvm_parse(t.ps, dev, (const char*)t.text.p, tc.bytes, h->m, nullptr, nullptr, RP_I64, nullptr,
+                             nullptr, 0, 0, st_comp, &rows, &nnz, &el);
+        if (r) return r;
+        const int64_t cap = cap_out >= 0 ? cap_out : out_cap(nnz);
+        if ((r = t.labels.ensure(8 * (size_t)std::max<int64_t>(rows, 1), dev)) ||
+            (r = stream_alloc_slot(h, t.s, rows, nnz, cap, 8, 4, c->indptr_type, c->indices_type)))
+            return r;
+        r = libsvm_parse(t.ps, dev, (const char*)t.text.p, tc.bytes, h->m, (double*)t.labels.p, t.s.ap.p, RP_I64,
+                         (int32_t*)t.s.aj.p, (float*)t.s.ax.p, rows, nnz, st_comp, &rows, &nnz, &el);
+        if (r == RP_ERR_INVALID && el >= 0) bad_line = lines_before(text, tc.b0) + el;
+        if (r) return r;
+        cks[(size_t)k].rows = rows;
+        cks[(size_t)k].nnz = nnz;
+        cks[(size_t)k].e0 = 0;
+        return RP_OK;
+    };
+    auto download = [&](int64_t k, TextSlot& t, int64_t* kn, bool* rd) -> int {
+        const StreamChunk& ck = cks[(size_t)k];
+        HIP_TRY(hipEventSynchronize(t.s.comp));
+        if (ck.rows > 0)
+            HIP_TRY(hipMemcpyAsync(labels + ck.r0, t.labels.p, 8 * (size_t)ck.rows, hipMemcpyDeviceToHost, st_down));
+        return stream_download(ck, t.s, nullptr, c, k == K - 1, st_down, 4, kn, rd);
+    };
+    std::thread up([&] {
+        if (hipSetDevice(dev) != hipSuccess) return sy.set_error(fail(RP_ERR_HIP, "hipSetDevice"));
+        for (int64_t k = 0; k < K; ++k) {
+            TextSlot& t = slots[k % ns];
+            if (!sy.wait([&] { return sy.launched >= k - ns + 1 || k < ns; })) return;
+            if (k >= ns && hipEventSynchronize(t.s.comp) != hipSuccess)
+                return sy.set_error(fail(RP_ERR_HIP, "event sync (upload)"));
+            if (int r = upload(k, t)) return sy.set_error(r);
+            sy.bump(sy.uploaded);
+        }
+    });
+    std::thread down([&] {
+        if (hipSetDevice(dev) != hipSuccess) return sy.set_error(fail(RP_ERR_HIP, "hipSetDevice"));
+        for (int64_t k = 0; k < K; ++k) {
+            if (!sy.wait([&] { return sy.launched > k; })) return;
+            bool rd = false;
+            if (int r = download(k, slots[k % ns], &knnz[(size_t)k], &rd)) return sy.set_error(r);
+            redo[(size_t)k] = rd;
+            sy.bump(sy.downloaded);
+        }
+    });
+    int64_t rows_total = 0;
+    for (int64_t k = 0; k < K && sy.err == RP_OK; ++k) {
+        if (!sy.wait([&] { return sy.uploaded > k && sy.downloaded >= k - ns + 1; })) break;
+        TextSlot& t = slots[k % ns];
+        if ((rc = parse(k, t, -1))) {
+            sy.set_error(rc);
+            break;
+        }
+        cks[(size_t)k].r0 = rows_total;
+        rows_total += cks[(size_t)k].rows;
+        if (rows_total > cap_rows) {
+            sy.set_error(fail(RP_ERR_CAPACITY, "more than %lld rows (cap_rows)", (long long)cap_rows));
+            break;
+        }
+        if ((rc = stream_project(h, cks[(size_t)k], t.s, order, RP_F32, c->indptr_type, c->indices_type,
+                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp))) {
+            sy.set_error(rc);
+            break;
+        }
+        sy.bump(sy.launched);
+    }
+    up.join();
+    down.join();
+    if (sy.err != RP_OK) {
+        (void)hipStreamSynchronize(st_comp);
+        cleanup();
+        g_err = sy.msg;
+        if (err_line) *err_line = bad_line;
+        if (sy.err == RP_ERR_CAPACITY) *n_rows = rows_total;
+        return sy.err;
+    }
+    // chunks whose entries exceeded their slot: parsed and projected again alone, exact size
+    int64_t base = 0, total = 0;
+    for (int64_t k = 0; k < K; ++k) total += knnz[(size_t)k];
+    rc = RP_OK;
+    for (int64_t k = 0; k < K && rc == RP_OK; base += knnz[(size_t)k], ++k) {
+        if (!redo[(size_t)k]) continue;
+        TextSlot& t = slots[0];
+        const int64_t r0 = cks[(size_t)k].r0;
+        if ((rc = upload(k, t)) || (rc = parse(k, t, knnz[(size_t)k]))) break;
+        cks[(size_t)k].r0 = r0;
+        unsigned long long tot0 = (unsigned long long)base;
+        if (hipMemcpyAsync(totbuf.p, &tot0, 8, hipMemcpyHostToDevice, st_comp) != hipSuccess) {
+            rc = fail(RP_ERR_HIP, "memcpy");
+            break;
+        }
+        if ((rc = stream_project(h, cks[(size_t)k], t.s, order, RP_F32, c->indptr_type, c->indices_type,
+                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp)))
+            break;
+        int64_t kk = 0;
+        bool rd = false;
+        rc = download(k, t, &kk, &rd);
+        if (rc == RP_OK && (rd || kk != knnz[(size_t)k])) rc = fail(RP_ERR_HIP, "chunk recompute mismatch");
+    }
+    (void)hipStreamSynchronize(st_comp);
+    cleanup();
+    if (rc) return rc;
+    *n_rows = rows_total;
     if (total_nnz) *total_nnz = total;
     if (total > c->capacity)
         return fail(RP_ERR_CAPACITY, "output capacity %lld < nnz %lld", (long long)c->capacity, (long long)total);

@@ -23,7 +23,7 @@ import weakref
 
 import numpy as np
 
-__all__ = ["empty", "pool_stats"]
+__all__ = ["empty", "pool_stats", "device_numa_node", "bind_to_device_numa"]
 
 _MIN_POOLED = 1 << 20          # smaller requests: np.empty (malloc's own heap reuses them)
 _GRAIN = 2 << 20               # mapping sizes are multiples of 2 MiB
@@ -99,3 +99,52 @@ def pool_stats() -> dict:
     with _lock:
         _drain_locked()
         return dict(_stats, idle_bytes=_idle_bytes, idle_mappings=sum(len(v) for v in _free.values()))
+
+
+def device_numa_node(device: int):
+    """NUMA node of a GPU's PCIe attachment (sysfs), or None when it cannot be determined."""
+    try:
+        import torch
+
+        pr = torch.cuda.get_device_properties(device)
+        bus, dev = getattr(pr, "pci_bus_id", None), getattr(pr, "pci_device_id", None)
+        if bus is None or dev is None:
+            return None
+        dom = int(getattr(pr, "pci_domain_id", 0) or 0)
+        with open(f"/sys/bus/pci/devices/{dom:04x}:{int(bus):02x}:{int(dev):02x}.0/numa_node") as f:
+            node = int(f.read().strip())
+        return node if node >= 0 else None
+    except Exception:  # noqa: BLE001 - sysfs layouts vary; binding is an optimisation only
+        return None
+
+
+def _cpulist(text: str) -> set:
+    cpus = set()
+    for part in text.strip().split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus
+
+
+def bind_to_device_numa(device: int) -> dict:
+    """Restrict this process to the CPUs of its GPU's NUMA node (when the node is known and shares
+    CPUs with the current affinity), so host buffers it allocates and first-touches afterwards
+    (pinned staging, result arrays) sit next to the GPU's PCIe root: with 8 ranks streaming host
+    CSR at once, every rank then draws on its own socket's DRAM channels. Returns what was done."""
+    node = device_numa_node(device)
+    if node is None:
+        return {"numa_node": None, "bound_cpus": None}
+    try:
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            want = _cpulist(f.read())
+        have = os.sched_getaffinity(0)
+        cpus = want & have
+        if not cpus:
+            return {"numa_node": node, "bound_cpus": None}
+        os.sched_setaffinity(0, cpus)
+        return {"numa_node": node, "bound_cpus": len(cpus)}
+    except OSError:
+        return {"numa_node": node, "bound_cpus": None}

@@ -23,7 +23,7 @@ from . import _native as nat
 from . import hostmem
 
 __all__ = ["parse_device", "parse_bytes", "iter_chunks", "split_range", "load_libsvm", "project_libsvm",
-           "libsvm_to_parquet", "partition_ids"]
+           "project_text_stream", "libsvm_to_parquet", "partition_ids"]
 
 DEFAULT_CHUNK = 256 << 20
 
@@ -188,6 +188,51 @@ def project_libsvm(path: str, projector, chunk_bytes: int = DEFAULT_CHUNK, order
             Cp = Cp.to(torch.int32)
         C = sp.csr_matrix((_download(Cx[:k]), _download(Cj[:k]), _download(Cp)), shape=(rows, projector.p))
         yield partition_ids(partition_base + ci, rows), _download(labels), C
+
+
+def project_text_stream(text, projector, order: str = "sorted", chunk_bytes: int = 64 << 20, out=None,
+                        out_index_dtype=None):
+    """Boundary 3 in one native call (rp_libsvm_project_stream): libsvm text in host memory (a uint8
+    numpy array, bytes or a mapped file's memoryview) -> chunks of whole lines uploaded, parsed and
+    projected on the GPU with upload, compute and download overlapped -> host arrays
+    ``(labels f64, indptr, indices, data f32)`` of ``X @ R`` for every row of the text.
+
+    ``out``: optional preallocated ``(labels, indptr, indices, data)`` host arrays (pinned or
+    pageable; capacities = their lengths) -- the steady-state form, nothing allocated per call.
+    Without it the capacities come from counting newlines and ':' in the text, with one exact retry."""
+    a = np.frombuffer(text, dtype=np.uint8) if not isinstance(text, np.ndarray) else text.reshape(-1).view(np.uint8)
+    lib = nat.load()
+    odx = {"sorted": nat.RP_ORDER_SORTED, "scipy": nat.RP_ORDER_SCIPY}[order]
+    if out is None:
+        rows_cap = int(np.count_nonzero(a == 10)) + 1
+        items = int(np.count_nonzero(a == 58))
+        exp = items * projector.nnz / max(projector.m, 1)
+        cap = int(1.05 * exp + 8 * np.sqrt(exp + 1)) + 65536
+    else:
+        rows_cap, cap = out[0].size, out[2].size
+    for _ in range(2):
+        if out is None:
+            it = np.dtype(out_index_dtype or (np.int32 if cap < 2**31 else np.int64))
+            o = (np.empty(rows_cap, np.float64), np.empty(rows_cap + 1, it), np.empty(max(cap, 1), it),
+                 np.empty(max(cap, 1), np.float32))
+        else:
+            o = out
+        labels, ip, ix, dx = o
+        co = nat.CsrOut(ip.ctypes.data, nat.idx_code(ip.dtype), ix.ctypes.data, nat.idx_code(ix.dtype),
+                        dx.ctypes.data, int(dx.size if cap > 0 else 0))
+        n, k, el = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(-1)
+        rc = lib.rp_libsvm_project_stream(projector._h, ctypes.c_void_p(a.ctypes.data), int(a.size), odx,
+                                          int(chunk_bytes), ctypes.c_void_p(labels.ctypes.data), int(labels.size),
+                                          ctypes.byref(co), ctypes.byref(n), ctypes.byref(k), ctypes.byref(el))
+        if rc == nat.RP_ERR_INVALID and el.value >= 0:
+            raise LibsvmFormatError(lib.rp_last_error().decode(), int(el.value))
+        if rc == nat.RP_ERR_CAPACITY and out is None and k.value > cap:
+            cap = int(k.value)
+            continue
+        nat.check(rc)
+        rows, nnz = int(n.value), int(k.value)
+        return labels[:rows], ip[:rows + 1], ix[:nnz], dx[:nnz]
+    raise RuntimeError("capacity retry failed")
 
 
 def libsvm_to_parquet(path: str, projector, out_dir: str, chunk_bytes: int = DEFAULT_CHUNK, byte_range=None,

@@ -304,8 +304,13 @@ class Projector:
         nat.check(rc)
         return int(total.value) if sync else None
 
-    def workspace_bytes(self, n_rows: int, nnz_a: int = -1) -> int:
-        """Device workspace for ``project_device`` on n_rows rows / nnz_a entries (staging included)."""
+    def workspace_bytes(self, n_rows: int, nnz_a: int = -1, dtype=None) -> int:
+        """Device workspace for ``project_device`` on n_rows rows / nnz_a entries (staging included);
+        ``dtype`` (the compute type, float32 or float64) sizes the value parts for it, else for
+        float64."""
+        if dtype is not None and nnz_a >= 0:
+            code = nat.RP_F64 if np.dtype(str(dtype).replace("torch.", "")) == np.float64 else nat.RP_F32
+            return int(self._lib.rp_project_workspace_bytes_for(self._h, int(n_rows), int(nnz_a), code))
         return int(self._lib.rp_project_workspace_bytes(self._h, int(n_rows), int(nnz_a)))
 
     def plan(self, n_rows: int, nnz_a: int = -1) -> dict:

@@ -90,3 +90,32 @@ def test_sharded_projector_two_ranks(tmp_path):
     assert np.array_equal(np.concatenate(labels), lab.astype(np.float32))
     assert np.array_equal(C.indptr, Xp) and np.array_equal(C.indices, Xj)
     assert np.array_equal(C.data, Xx.astype(np.float64))
+
+
+def test_bench_host_boundary_two_ranks():
+    """bench.py --boundary host at N = 2 (rehearsed with both ranks on cuda:0 over gloo): every rank
+    streams its own host shard through rp_project_stream, the wall time is the max over ranks, and
+    every rank's sampled rows equal the oracle's (the N = 8 driver path is the same code over RCCL)."""
+    import json
+
+    world = 2
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), WORLD_SIZE=str(world),
+               RP_BENCH_REHEARSE_ONE_GPU="1")
+    bench = os.path.join(os.path.dirname(HERE), "bench.py")
+    args = [sys.executable, bench, "--boundary", "host", "--rows", "3000000", "--m", "2000000", "--steps", "2",
+            "--warmup", "1", "--chunk-rows", "1000000"]
+    procs = [subprocess.Popen(args, env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=240))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert all(p.returncode == 0 for p in procs), "\n".join(o[1][-3000:] for o in outs)
+    line = json.loads([ln for ln in outs[0][0].splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["config"]["boundary"] == "host"
+    assert line["verified"]["sample_bitexact_vs_oracle"] and line["verified"]["indptr_ok"]
+    assert line["value"] > 0 and not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]

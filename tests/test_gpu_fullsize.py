@@ -4,8 +4,9 @@
   columns, scipy and sorted row order);
 * configs[2]: all 1,077,345,288 rows (9x KDD2012) on ONE GPU — output nnz > 2^31, so int64
   output indptr;
-* configs[3]: power-law rows with exactly 100 nnz over the real m = 10,000,000 features -> 1024
-  (4M rows: the 200M-row bench size does not leave room for the checks).
+* configs[3]: power-law rows with exactly 100 nnz over the real m = 10,000,000 features -> 1024,
+  at its full 200,000,000 rows in one call (2.0e10 input entries, 6.3e9 output entries: int64
+  input and output indptr, entries stored past 2^31 and 2^32), and at 4M rows in both orders.
 
 Whole outputs are checked on the device (indptr from 0 to nnz and monotone, columns in [0, p),
 rows ascending for the sorted order); >= 64k rows spread over the matrix (plus the last rows, past
@@ -46,7 +47,7 @@ def project(P, Ap, Aj, Ax, order="scipy", slack=1.02):
     dev = Aj.device
     n = Ap.numel() - 1
     nnz_a = int(Aj.numel())
-    ws = torch.empty(P.workspace_bytes(n, nnz_a), dtype=torch.uint8, device=dev)
+    ws = torch.empty(P.workspace_bytes(n, nnz_a, dtype=Ax.dtype), dtype=torch.uint8, device=dev)
     cap = int(slack * nnz_a * P.nnz / P.m) + 65536
     for _ in range(2):
         Cp = torch.empty(n + 1, dtype=torch.int64 if cap >= 2**31 else torch.int32, device=dev)
@@ -147,5 +148,33 @@ def test_configs3_real_m():
         check_csr_on_device(Cp, Cj, nnz, p, sorted_rows=(order == "sorted"))
         assert check_rows_vs_oracle(sample_rows(n, 65536), Ap, Aj, Ax, Cp, Cj, Cx, R, order=order) > 1_000_000
         del Cp, Cj, Cx
+    P.close()
+    torch.cuda.empty_cache()
+
+
+def test_configs3_full_size():
+    """BASELINE configs[3] at its real size: 200,000,000 power-law rows x 10,000,000, exactly 100
+    nnz per row -> 1024, one rp_project_device call on the tile pipeline with int64 input and output
+    indptr (2.0e10 input entries, ~6.3e9 output entries). Whole output checked on the device in
+    bounded chunks; >= 64k sampled rows bit-exact against the oracle, including rows stored past
+    2^31 and past 2^32 output entries."""
+    import torch
+
+    torch.cuda.empty_cache()
+    m, p, n = 10_000_000, 1024, 200_000_000
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    P = Projector(R)
+    Ap, Aj, Ax = synth.kdd_rows_device(n, m, seed=5, dist="powerlaw", mean_extra=-100.0, indptr_dtype=torch.int64)
+    assert Ap.dtype == torch.int64 and Aj.numel() == 100 * n
+    assert P.plan(n, Aj.numel())["pipeline"] == "tile"
+    Cp, Cj, Cx, nnz = project(P, Ap, Aj, Ax, slack=1.0)
+    assert Cp.dtype == torch.int64 and nnz > 2**32 and 30 < nnz / n < 33
+    check_csr_on_device(Cp, Cj, nnz, p)
+    rows = sample_rows(n, 65536)
+    off = Cp[torch.as_tensor(rows, device=Cp.device)]
+    assert int((off > 2**31).sum().item()) > 40_000 and int((off > 2**32).sum().item()) > 15_000, \
+        "the sample must reach rows stored past 2^31 and 2^32 output entries"
+    assert check_rows_vs_oracle(rows, Ap, Aj, Ax, Cp, Cj, Cx, R) > 2_000_000
+    del Ap, Aj, Ax, Cp, Cj, Cx
     P.close()
     torch.cuda.empty_cache()

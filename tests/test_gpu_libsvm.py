@@ -7,7 +7,7 @@ import scipy.sparse as sp
 from oracle import smmp
 from oracle.libsvm_ref import ParseError, parse_text
 from randomprojection_amd import Projector, srp_matrix as sm
-from randomprojection_amd.libsvm import LibsvmFormatError, parse_bytes, project_libsvm
+from randomprojection_amd.libsvm import LibsvmFormatError, parse_bytes, parse_device, project_libsvm, project_text_stream
 
 pytestmark = pytest.mark.gpu
 
@@ -141,3 +141,83 @@ def test_every_java_double_literal_exact():
     assert bad.size == 0, [(lines[i].split()[0], labels[i], lab[i]) for i in bad[:5]]
     assert np.array_equal(X.indptr, ip) and np.array_equal(X.indices, ix)
     assert same(X.data, vx)
+
+
+@pytest.mark.parametrize("order", ["sorted", "scipy"])
+@pytest.mark.parametrize("chunk", [4096, 100_000, 64 << 20])
+def test_project_text_stream_vs_oracle(order, chunk):
+    """Boundary 3 in one native call (rp_libsvm_project_stream): chunks of whole lines overlapped
+    upload / parse + projection / download; comments, blank lines, odd spacing, a last line without
+    its newline, chunks smaller than a line; every row's label, indices and value bits equal the
+    restated Spark parser + scipy kernel."""
+    rng = np.random.default_rng(23)
+    m, p = 200_000, 1024
+    txt = random_text(rng, 7001, m) + b"1 5:2.5 77:-1e-3"  # no trailing newline
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    P = Projector(R)
+    lab, ip, ix, vx = parse_text(txt, m)
+    A = sp.csr_matrix((vx, ix, ip), shape=(len(lab), m))
+    Cp, Cj, Cx, _, _ = smmp.matmat(A, R)
+    if order == "sorted":
+        Cj, Cx = smmp.sorted_rows(Cp, Cj, Cx)
+    labels, gp, gj, gx = project_text_stream(txt, P, order=order, chunk_bytes=chunk)
+    assert same(labels, lab)
+    assert np.array_equal(gp, Cp) and np.array_equal(gj, Cj) and same(gx, Cx)
+
+
+def test_project_text_stream_synthetic_kdd_text():
+    """Text written on the GPU from KDD-shaped rows (rp_synth_libsvm_device, 6-17 digit values):
+    streamed in 1 MB chunks into preallocated arrays, the result equals parsing the whole text in
+    one device call and projecting it with rp_project_device; sampled lines equal the oracle."""
+    import torch
+
+    from randomprojection_amd import synth
+
+    m, p, n = 2_000_000, 4096, 150_000
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    P = Projector(R)
+    Ap, Aj, Ax = synth.kdd_rows_device(n, m, seed=9)
+    t, off = synth.libsvm_text_device(Ap, Aj, seed=3)
+    text = t.cpu().numpy()
+    offs = off.cpu().numpy()
+    assert offs[-1] == text.size and text[-1] == 10
+    labels, gp, gj, gx = project_text_stream(text, P, order="scipy", chunk_bytes=1 << 20)
+    assert labels.size == n
+    # the same text parsed whole on the device, then projected device-resident
+    dl, dp, dj, dx = parse_device(t, int(t.numel()), m)
+    assert torch.equal(dj, Aj)  # the synthetic text carries the generator's columns
+    nnz = int(dj.numel())
+    cap = int(1.1 * nnz * P.nnz / P.m) + 4096
+    Cp = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+    Cj = torch.empty(cap, dtype=torch.int32, device="cuda")
+    Cx = torch.empty(cap, dtype=torch.float32, device="cuda")
+    k = P.project_device(dp, dj, dx, Cp, Cj, Cx, nnz_a=nnz)
+    assert same(labels, dl.cpu().numpy())
+    assert np.array_equal(gp, Cp.cpu().numpy()) and np.array_equal(gj, Cj[:k].cpu().numpy())
+    assert same(gx, Cx[:k].cpu().numpy())
+    rows = np.sort(np.random.default_rng(1).choice(n, 500, replace=False))
+    sample = b"".join(text[offs[r]:offs[r + 1]].tobytes() for r in rows)
+    l_ref, p_ref, j_ref, v_ref = parse_text(sample, m)
+    assert same(labels[rows], l_ref)
+    W = smmp.matmat(sp.csr_matrix((v_ref, j_ref, p_ref), shape=(rows.size, m)), R)
+    G = sp.csr_matrix((gx, gj, gp), shape=(n, p))[rows]
+    assert np.array_equal(G.indptr, W[0]) and np.array_equal(G.indices, W[1]) and same(G.data, W[2])
+
+
+def test_project_text_stream_errors():
+    """A malformed line reports its 0-based line number in the whole text (not in its chunk); too
+    small preallocated outputs give RP_ERR_CAPACITY."""
+    from randomprojection_amd import _native as nat
+
+    m = 1000
+    R = sm.projection_operand(sm.sparse_random_matrix(64, m, random_state=1))
+    P = Projector(R)
+    good = "".join(f"{i % 2} {i % 900 + 1}:1.5 {i % 900 + 50}:2\n" for i in range(5000))
+    txt = (good + "1 7:1 3:2\n" + good).encode()
+    with pytest.raises(LibsvmFormatError) as e:
+        project_text_stream(txt, P, chunk_bytes=4096)
+    assert e.value.line == 5000
+    small = (np.empty(10), np.empty(11, np.int32), np.empty(100, np.int32), np.empty(100, np.float32))
+    with pytest.raises(nat.RPError) as c:
+        project_text_stream(good.encode(), P, chunk_bytes=4096, out=small)
+    assert c.value.code == nat.RP_ERR_CAPACITY
