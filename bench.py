@@ -1,7 +1,8 @@
 """Benchmark: rows/s projected (KDD2012 54,686,452 -> 4096, R from SparseRandomProjection(random_state=123)).
 
-One step = one pass of the hot path (C = A @ R, librp's single-launch HIP SpGEMM) over the whole
-workload, inputs resident in HBM when timing starts (boundary 1 of SURVEY.md §8(d)):
+One step = one pass of the hot path (C = A @ R: one rp_project_device call, i.e. every kernel of the
+pipeline it runs) over the whole workload, inputs resident in HBM when timing starts
+(boundary 1 of SURVEY.md §8(d)); --boundary host / libsvm time boundaries 2 and 3 instead:
   N=1: BASELINE.json configs[1] — the full KDD2012 train shape, 119,705,032 synthetic rows
        (per-row nnz 1 + Poisson(10), distinct uniform columns, values 1.0) on one MI355X.
   N>1: weak scaling — every rank projects its own 119,705,032-row shard (configs[2]'s
@@ -11,6 +12,7 @@ workload, inputs resident in HBM when timing starts (boundary 1 of SURVEY.md §8
 Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
 
     python bench.py [--config kdd|kdd9x|cfg4] [--gpus N] [--steps K] [--warmup W] [--rows R]
+                    [--boundary device|host|libsvm]
 """
 from __future__ import annotations
 
@@ -284,7 +286,7 @@ def main():
     # HBM bytes per step and the L2 hit rate of the main kernel. A traffic file applies only when
     # it names the same rows, column distribution, pipeline and librp source hash: a kernel change
     # without a fresh profile reports traffic null, never an old number.
-    traffic, l2_hit, traffic_file = None, None, None
+    traffic, traffic_file, tj_used = None, None, {}
     cands = [args.traffic_json] + sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")))
     for f in cands:
         try:
@@ -294,13 +296,14 @@ def main():
         if (tj.get("rows") == args.rows and tj.get("dist") == args.dist and tj.get("src_sha16") == SRC_SHA16
                 and tj.get("pipeline") == plan["pipeline"] and tj.get("staged") == plan["staged"]
                 and tj.get("staged_this_call", staged_run) == staged_run):
-            traffic, l2_hit = tj.get("hbm_bytes_per_launch"), tj.get("l2_hit_rate_main_kernel")
+            traffic, tj_used = tj.get("hbm_bytes_per_launch"), tj
             traffic_file = os.path.relpath(f, ROOT)
             break
-    # the ceiling that binds this kernel: one random R-descriptor gather per A entry, each a full
-    # 128-B line fill; measured on MI355X at ~55 G random lines/s for any table from 32 MB to 2 GB,
-    # any load flavour or allocation (profiles/r01_probe_gather_*.json)
-    gathers_per_s = nnz_a / (kernel_ms * 1e-3)
+    # L2 behaviour from the same PMC session (null without one for these sources): the hit rate of
+    # the kernel that gathers R's descriptors (the staged gather kernel when it ran, else the main
+    # kernel), the main kernel's own, and the gathering kernel's measured L2->fabric read requests
+    # per second against the ~55 G random lines/s ceiling (scripts/probes/gather_probe*.hip)
+    req = tj_used.get("gather_kernel_read_requests_G_per_s")
 
     if rank == 0:
         total_rows = total_rows_cfg if cfg.get("strong") else args.rows * world
@@ -325,13 +328,16 @@ def main():
                          "kernel_ms": kernel_ms, "bytes_per_row": b_row,
                          "model": "B_row=(4+8a)+a(8+8r)+(4+8c)", "a": a, "r": rbar, "c": c,
                          "traffic_source": f"rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per step, {traffic_file}",
-                         "l2_hit_rate_r_gathers": l2_hit,
+                         "l2_hit_rate_r_gathers": tj_used.get("l2_hit_rate_r_gathers"),
+                         "r_gather_kernel": tj_used.get("gather_kernel"),
+                         "l2_hit_rate_main_kernel": tj_used.get("l2_hit_rate_main_kernel"),
                          "pipeline": plan, "librp_src_sha16": SRC_SHA16,
                          "step_kernels": step_kernels(plan, staged_run),
                          "traffic_GBps": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
                          "random_line_ceiling_G_per_s": RANDOM_LINE_CEILING / 1e9,
-                         "gathers_G_per_s": gathers_per_s / 1e9,
-                         "frac_of_random_line_ceiling": gathers_per_s / RANDOM_LINE_CEILING},
+                         "r_gather_kernel_line_requests_G_per_s": req,
+                         "r_gather_kernel_frac_of_random_line_ceiling":
+                             (req * 1e9 / RANDOM_LINE_CEILING) if req else None},
             "cpu_baseline": cpu,
             "verified": check,
             "r_setup_s": t_r,
@@ -396,6 +402,16 @@ def _barrier(dev):
         dist.barrier()
 
 
+def _r_host(args, R_host):
+    """R on the host for the oracle check after the clock: rank 0 has it; other ranks received only
+    the packed device image over the broadcast and regenerate it (sklearn-identical, seeded)."""
+    if R_host is not None:
+        return R_host
+    from randomprojection_amd import srp_matrix as sm
+
+    return sm.projection_operand(sm.sparse_random_matrix(args.p, args.m, random_state=123))
+
+
 def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
     """Boundary 2: host CSR in -> host CSR out, PCIe-inclusive, through
     rp_project_stream (chunk k+1 uploading while chunk k projects and chunk k-1 downloads). The
@@ -445,7 +461,7 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
     rng = np.random.default_rng(20261016 + rank)
     rows = np.sort(rng.choice(n, size=min(4096, n), replace=False))
     A = sp.csr_matrix((ax, aj, ap), shape=(n, args.m))[rows]
-    Wp, Wj, Wx, _, _ = smmp.matmat(A, R_host)
+    Wp, Wj, Wx, _, _ = smmp.matmat(A, _r_host(args, R_host))
     if order == "sorted":
         Wj, Wx = smmp.sorted_rows(Wp, Wj, Wx)
     C = sp.csr_matrix((cx, cj, cp), shape=(n, args.p))[rows]
@@ -540,7 +556,7 @@ def bench_libsvm(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
     sample = b"".join(text[offs[r]:offs[r + 1]].tobytes() for r in rows)
     l_ref, p_ref, j_ref, v_ref = parse_text(sample, args.m)
     A = sp.csr_matrix((v_ref, j_ref, p_ref), shape=(rows.size, args.m))
-    Wp, Wj, Wx, _, _ = smmp.matmat(A, R_host)
+    Wp, Wj, Wx, _, _ = smmp.matmat(A, _r_host(args, R_host))
     if order == "sorted":
         Wj, Wx = smmp.sorted_rows(Wp, Wj, Wx)
     C = sp.csr_matrix((cx, cj, cp), shape=(n, args.p))[rows]

@@ -6,20 +6,23 @@
 // row-major with the contraction index m contiguous ("NT" GEMM), the layout the MFMA operand
 // fragments want: a lane's A and B elements are consecutive in memory.
 //
-//   bf16: v_mfma_f32_32x32x16_bf16 — bf16 operands, f32 accumulate, f32 result.
-//   f32:  v_mfma_f32_32x32x2_f32   — exact f32 products (gfx950 has no xf32), f32 accumulate.
+//   bf16: bf16 operands, f32 accumulate, f32 result (v_mfma_f32_16x16x32_bf16 / _32x32x16_bf16).
+//   f32:  exact f32 products (gfx950 has no xf32), f32 accumulate (v_mfma_f32_16x16x4_f32 / _32x32x2_f32).
 //
-// Block tile 128 x 128, 4 waves (2 x 2), each wave 64 x 64 = 2 x 2 MFMA tiles of 32 x 32. K step
-// 128 bytes of a row (64 bf16 / 32 f32): the next step's tiles are loaded global -> registers
-// while the current step's MFMAs run, then written to the other LDS buffer (two buffers, one
-// barrier per step). LDS rows are 128 B (8 chunks of 16 B) stored XOR-swizzled (chunk c of row r
-// at c ^ (r & 7)) so a wave's 16-B fragment reads of 8 consecutive rows hit distinct banks.
-// f32: the K order inside a step is permuted (lane half h takes k = 16h + t for MFMA t) so every
-// lane reads 64 contiguous bytes per operand per step; the sum is over the same products.
-// Block -> tile map is XCD-aware: XCD x (workgroup i runs on XCD i % 8) takes the M tiles
+// Two kernel families (rp_dense_set_variant picks one for measurements):
+//  * dense_glds_kernel (variant 10, the bf16 default): 256 x 256 tile, 8 waves of 128 x 64, 16 x 16
+//    MFMAs, operands staged global -> LDS by global_load_lds_dwordx4 (no VGPR round trip), XOR
+//    swizzle applied on the source address, two K-tile buffers with the next K-tile in flight during
+//    this one's MFMAs (description above the kernel);
+//  * dense_nt_kernel (variants 0-9; variant 5 = 256 x 256, 8 waves, 32 x 32 MFMAs, two LDS stages, is
+//    the f32 default): the next K step loaded global -> registers during the MFMAs, then written to
+//    the other LDS buffer (one barrier per step); LDS rows of 128 B XOR-swizzled (chunk c of row r at
+//    c ^ (r & 7)); f32 permutes the K order inside a step so every lane reads 64 contiguous bytes.
+// Block -> tile map is XCD-aware in both: XCD x (workgroup i runs on XCD i % 8) takes the M tiles
 // congruent to x mod 8 and walks each M tile's N tiles back to back, so an X tile is fetched from
 // HBM once and re-read from that XCD's L2.
 #include <atomic>
+#include <type_traits>
 
 #include "rp_common.h"
 
@@ -209,6 +212,132 @@ dense_nt_kernel(const T* __restrict__ A, const T* __restrict__ B, float* __restr
         }
 }
 
+// LDS-direct staging (the default): tile 256 x 256, K-tile = 128 B of every row (64 bf16 / 32 f32),
+// 8 waves (2 M x 4 N), each wave 128 x 64 of C as 8 x 4 tiles of 16 x 16.
+//   bf16: v_mfma_f32_16x16x32_bf16, lane l: A[row l & 15][k 8(l >> 4) .. +7] (16 B), the same for B's
+//         row = C's column;
+//   f32:  v_mfma_f32_16x16x4_f32 (exact f32 products), lane l: A[row l & 15][k = l >> 4]; a lane reads
+//         16 B = 4 consecutive k and feeds element e to MFMA e, so MFMA (s, e) sums k = 16s + 4q + e
+//         over the lane groups q — a permutation of the K-tile, the same for A and B.
+//   C (both): col l & 15, rows 4(l >> 4) + r.
+// Operands go global -> LDS with global_load_lds_dwordx4 (16 B per lane, no VGPR round trip): per
+// K-tile 4 instructions per thread for A and 4 for B. The LDS image is lane-linear (128-B rows of 8
+// chunks); the XOR swizzle (chunk c of row r holds global chunk c ^ (r & 7)) is applied on the
+// per-lane SOURCE address, so a 16-lane group's fragment reads (16 rows, one chunk) hit 16 distinct
+// 16-B bank slots. Two K-tile buffers: K-tile t + 1 is issued before K-tile t's MFMAs, one vmcnt(0) +
+// barrier per K-tile. All LDS in ONE __shared__ array (a second one makes hipcc wait vmcnt(0) before
+// the first ds_read). Rows past M / N are read (clamped) and never stored.
+typedef short bf16x8s __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <bool BF16>
+__global__ void __launch_bounds__(512)
+dense_glds_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, float* __restrict__ C,
+                  int64_t M, int N, int K, int64_t ldc, unsigned m_tiles, unsigned n_tiles) {
+    constexpr int BM = 256, BN = 256, KC = 8;       // KC: 16-B chunks per 128-B row slice
+    constexpr int ES = BF16 ? 2 : 4, KT = 128 / ES;  // element size, elements per K-tile
+    __shared__ uint4 lds[2 * (BM + BN) * KC];       // 2 x 64 KB
+    const unsigned bi = blockIdx.x, xcd = bi & 7u, j = bi >> 3;
+    const unsigned mt = (j / n_tiles) * 8u + xcd, nt = j % n_tiles;
+    if (mt >= m_tiles) return;  // uniform
+    const int64_t m0 = (int64_t)mt * BM;
+    const int n0 = (int)nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 2, wn = w & 3;
+    const int steps = K / KT;
+    // staging sources: instruction i moves LDS chunks [i * 512 + 64 w, + 64) of the A (B) image
+    const int srow = tid >> 3, sch = tid & 7, sxc = sch ^ (srow & 7);
+    const char* ga[4];
+    const char* gb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t ra = std::min<int64_t>(m0 + i * 64 + srow, M - 1);
+        const int rb = std::min(n0 + i * 64 + srow, N - 1);
+        ga[i] = reinterpret_cast<const char*>(Av) + (ra * (int64_t)K + sxc * (16 / ES)) * ES;
+        gb[i] = reinterpret_cast<const char*>(Bv) + ((int64_t)rb * K + sxc * (16 / ES)) * ES;
+    }
+    auto stage = [&](int kt, int buf) {
+        uint4* base = lds + buf * (BM + BN) * KC;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds(ga[i] + (int64_t)kt * 128, base + i * 512 + 64 * w, 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds(gb[i] + (int64_t)kt * 128, base + BM * KC + i * 512 + 64 * w, 16, 0, 0);
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fq = lane >> 4;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < steps; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < steps) stage(kt + 1, cur ^ 1);  // buffer cur ^ 1: last read before the previous barrier
+        const uint4* sa = lds + cur * (BM + BN) * KC;
+        const uint4* sb = sa + BM * KC;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int cc = 4 * s + fq;
+            uint4 bfr[4];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int r = wn * 64 + ni * 16 + fr;
+                bfr[ni] = sb[r * KC + (cc ^ (r & 7))];
+            }
+#pragma unroll
+            for (int mi = 0; mi < 8; ++mi) {
+                const int r = wm * 128 + mi * 16 + fr;
+                const uint4 afr = sa[r * KC + (cc ^ (r & 7))];
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    if constexpr (BF16) {
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8s, afr), __builtin_bit_cast(bf16x8s, bfr[ni]), acc[mi][ni], 0, 0, 0);
+                    } else {
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(afr.x), __uint_as_float(bfr[ni].x),
+                                                                          acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(afr.y), __uint_as_float(bfr[ni].y),
+                                                                          acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(afr.z), __uint_as_float(bfr[ni].z),
+                                                                          acc[mi][ni], 0, 0, 0);
+                        acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(afr.w), __uint_as_float(bfr[ni].w),
+                                                                          acc[mi][ni], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int c = n0 + wn * 64 + ni * 16 + fr;
+            if (c >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + wm * 128 + mi * 16 + 4 * fq + r;
+                if (row < M) C[row * ldc + c] = acc[mi][ni][r];
+            }
+        }
+}
+
+template <bool BF16>
+int launch_dense_glds(const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
+                      hipStream_t st) {
+    const unsigned m_tiles = (unsigned)((n + 255) / 256), n_tiles = (unsigned)((p + 255) / 256);
+    const uint64_t blocks = (uint64_t)((m_tiles + 7) / 8) * 8ull * n_tiles;
+    if (blocks >= (1ull << 31)) return fail(RP_ERR_UNSUPPORTED, "too many rows for one launch");
+    hipLaunchKernelGGL((dense_glds_kernel<BF16>), dim3((unsigned)blocks), dim3(512), 0, st, X, G, Y, n, (int)p, (int)m,
+                       ldy, m_tiles, n_tiles);
+    HIP_TRY(hipGetLastError());
+    return RP_OK;
+}
+
 template <typename T, int WM, int WN, int TM, int TN, int STAGES, int DEPTH = 1>
 int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
                  hipStream_t st) {
@@ -225,10 +354,13 @@ int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, i
 // tile variants (RP_DENSE_VARIANT, measurements): 0 = 128x128 2 stages, 1 = 128x128 1 stage,
 // 2 = 256x128 1 stage, 3 = 128x256 2 stages (8 waves), 4 = 256x256 1 stage (8 waves), 5 = 256x256
 // 2 stages (128 KB LDS, 8 waves)
-constexpr int kDenseVariant = 5;  // 256 x 256, two LDS stages (measured best of 0-5, profiles/r02_dense_variants.json)
+// defaults per dtype: bf16 LDS-direct 256 x 256 (1221 TF vs 355 for variant 5, profiles/r03_dense_*),
+// f32 the register-staged 256 x 256 two-stage tile until the LDS-direct f32 form measures faster
+constexpr int kDenseVariantBf16 = 10, kDenseVariantF32 = 5;
 template <typename T>
 int dispatch_dense(int v, const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
                    hipStream_t st) {
+    if (v == 10) return launch_dense_glds<std::is_same<T, uint16_t>::value>(X, G, Y, n, m, p, ldy, st);
     switch (v) {
         case 1: return launch_dense<T, 2, 2, 2, 2, 1>(X, G, Y, n, m, p, ldy, st);
         case 2: return launch_dense<T, 2, 2, 4, 2, 1>(X, G, Y, n, m, p, ldy, st);
@@ -248,7 +380,7 @@ std::atomic<int> g_dense_variant{-1};  // rp_dense_set_variant (measurements); -
 }  // namespace
 
 extern "C" int rp_dense_set_variant(int32_t variant) {
-    if (variant < -1 || variant > 7) return fail(RP_ERR_INVALID, "variant must be -1 (default) or 0..7");
+    if (variant < -1 || variant > 10) return fail(RP_ERR_INVALID, "variant must be -1 (default) or 0..10");
     g_dense_variant.store(variant, std::memory_order_relaxed);
     return RP_OK;
 }
@@ -266,7 +398,7 @@ extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype,
     if (n == 0) return RP_OK;
     HIP_TRY(hipSetDevice(device));
     const int sv = g_dense_variant.load(std::memory_order_relaxed);
-    const int v = sv >= 0 ? sv : kDenseVariant;
+    const int v = sv >= 0 ? sv : (dtype == RP_BF16 ? kDenseVariantBf16 : kDenseVariantF32);
     hipStream_t st = (hipStream_t)stream;
     return dtype == RP_BF16 ? dispatch_dense<uint16_t>(v, X, G, Y, n, m, p, ldy, st)
                             : dispatch_dense<float>(v, X, G, Y, n, m, p, ldy, st);

@@ -110,6 +110,9 @@ def main():
                    staged_this_call=bench.get("staged_this_call"))
     mains = [k for k in MAIN_KERNELS if summary["kernels"].get(k, {}).get("avg_ms")]
     main_k = max(mains, key=lambda k: summary["kernels"][k]["avg_ms"]) if mains else None  # the one that ran
+    # the kernel that gathers R's descriptors: the staged gather when it ran, else the main kernel
+    gk = summary["kernels"].get("lpr_gather_kernel", {})
+    gather_k = "lpr_gather_kernel" if gk.get("avg_ms", 0) > 0.05 else main_k
     if "hbm_bytes" in summary["step"]:
         tj = {"tag": args.tag, "rows": args.rows, "dist": args.dist,
               "pipeline": plan.get("pipeline"), "staged": plan.get("staged"), "src_sha16": roof.get("librp_src_sha16"),
@@ -117,6 +120,10 @@ def main():
               "hbm_bytes_per_launch": summary["step"]["hbm_bytes"],
               "main_kernel": main_k,
               "l2_hit_rate_main_kernel": summary["kernels"].get(main_k, {}).get("l2_hit_rate"),
+              "gather_kernel": gather_k,
+              "l2_hit_rate_r_gathers": summary["kernels"].get(gather_k, {}).get("l2_hit_rate"),
+              "gather_kernel_read_requests_G_per_s": summary["kernels"].get(gather_k, {}).get("read_requests_G_per_s"),
+              "main_kernel_read_requests_per_launch": summary["kernels"].get(main_k, {}).get("read_requests"),
               "l2_hit_rate_step": summary["step"].get("l2_hit_rate"),
               "note": "per projection step (all kernels of rp_project_device)",
               "source": f"profiles/{args.tag}_summary.json"}

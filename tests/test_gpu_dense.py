@@ -50,13 +50,18 @@ def test_sparse_input():
     assert _rel(ours.transform(X), ref.transform(X)) < 1e-5
 
 
+@pytest.mark.parametrize("variant", [-1, 5, 10])
 @pytest.mark.parametrize("compute", ["fp32", "bf16"])
 @pytest.mark.parametrize("shape", [(1, 64, 1), (300, 4096, 200), (1000, 16384, 1024), (257, 192, 129)])
-def test_mfma_kernel_ragged_shapes(compute, shape):
-    """librp's MFMA GEMM on ragged tiles (rows / columns past the 128 x 128 block, m not a multiple
-    of the K step: padded) against an fp64 product of the same (bf16-rounded) operands."""
+def test_mfma_kernel_ragged_shapes(compute, shape, variant):
+    """librp's MFMA GEMM kernels (the default, the register-staged 256 x 256 tile and the LDS-direct
+    one) on ragged tiles (rows / columns past the block, m not a multiple of the K step: padded)
+    against an fp64 product of the same (bf16-rounded) operands."""
     import torch
+    from randomprojection_amd import _native as nat
     from randomprojection_amd.gaussian import dense_project_device
+
+    nat.check(nat.load().rp_dense_set_variant(variant))
 
     n, m, p = shape
     rng = np.random.default_rng(n + m + p)
@@ -69,4 +74,5 @@ def test_mfma_kernel_ragged_shapes(compute, shape):
     assert _rel(Y, ref) < 1e-5  # north_star fp32 tolerance (K = 16384 f32 fma chains: ~2e-6 measured)
     out = torch.full((n, p + 7), 7.0, device="cuda")[:, :p]  # a strided output view
     dense_project_device(X, C, out=out, compute=compute)
+    nat.check(nat.load().rp_dense_set_variant(-1))
     assert np.array_equal(out.cpu().numpy(), Y)

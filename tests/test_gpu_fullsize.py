@@ -158,15 +158,21 @@ def test_configs3_full_size():
     indptr (2.0e10 input entries, ~6.3e9 output entries). Whole output checked on the device in
     bounded chunks; >= 64k sampled rows bit-exact against the oracle, including rows stored past
     2^31 and past 2^32 output entries."""
+    import gc
+
     import torch
 
+    gc.collect()
     torch.cuda.empty_cache()
+    print("before configs[3]: free/total", torch.cuda.mem_get_info(), "allocated", torch.cuda.memory_allocated())
     m, p, n = 10_000_000, 1024, 200_000_000
     R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
     P = Projector(R)
     Ap, Aj, Ax = synth.kdd_rows_device(n, m, seed=5, dist="powerlaw", mean_extra=-100.0, indptr_dtype=torch.int64)
     assert Ap.dtype == torch.int64 and Aj.numel() == 100 * n
     assert P.plan(n, Aj.numel())["pipeline"] == "tile"
+    print("A ready: allocated", torch.cuda.memory_allocated(), "workspace",
+          P.workspace_bytes(n, Aj.numel(), dtype=Ax.dtype), P.workspace_bytes(n, Aj.numel()))
     Cp, Cj, Cx, nnz = project(P, Ap, Aj, Ax, slack=1.0)
     assert Cp.dtype == torch.int64 and nnz > 2**32 and 30 < nnz / n < 33
     check_csr_on_device(Cp, Cj, nnz, p)
