@@ -289,13 +289,14 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
 int rp_synth_libsvm_device(int device, int64_t n_rows, const int64_t* indptr, const int32_t* indices, uint64_t seed,
                            int64_t* line_offsets, char* text, int64_t cap_bytes, void* stream, int64_t* n_bytes);
 
-/* Dense Gaussian projection (BASELINE configs[4]): Y[n x p] (f32, row stride ldy) = X[n x m] .
- * G[p x m]^T for device arrays X and G of dtype RP_F32 (exact-f32 MFMA products, f32 accumulate) or
- * RP_BF16 (bf16 operands, f32 accumulate), both row-major, 16-byte aligned, m a multiple of 32
- * (f32) / 64 (bf16). Replaces sklearn GaussianRandomProjection.transform's X @ components_.T
- * (sklearn/random_projection.py:569-612) with a hand-written MFMA GEMM. Asynchronous on `stream`. */
+/* Dense Gaussian projection (BASELINE configs[4]): Y[n x p] (row stride ldy) = X[n x m] . G[p x m]^T
+ * for device arrays X and G of dtype RP_BF16 (bf16 operands, f32 accumulate, Y f32), RP_F32 (exact-f32
+ * MFMA products, f32 accumulate, Y f32) or RP_F64 (f64 MFMA, Y f64), both row-major, 16-byte aligned,
+ * m a multiple of 64 (bf16) / 32 (f32) / 16 (f64). Replaces sklearn GaussianRandomProjection.transform's
+ * X @ components_.T (sklearn/random_projection.py:569-612), computed in X's dtype as sklearn does,
+ * with hand-written MFMA GEMMs. Asynchronous on `stream`. */
 int rp_dense_project_device(int device, const void* X, int32_t dtype, int64_t n, int64_t m, const void* G,
-                            int64_t p, float* Y, int64_t ldy, void* stream);
+                            int64_t p, void* Y, int64_t ldy, void* stream);
 /* Library-wide tile variant of rp_dense_project_device (measurements): -1 = the default. */
 int rp_dense_set_variant(int32_t variant);
 

@@ -338,6 +338,107 @@ int launch_dense_glds(const void* X, const void* G, float* Y, int64_t n, int64_t
     return RP_OK;
 }
 
+// f64 (sklearn computes in X's dtype): v_mfma_f64_16x16x4_f64 — lane l supplies A[row l & 15][k = l >> 4]
+// (one double), C/D: col l & 15, row (l >> 4) + 4 r (NOT the f32 map). Tile 256 x 128, 8 waves (4 M x
+// 2 N) of 64 x 64 = 4 x 4 MFMA tiles (128 accumulator VGPRs); K-tile = 128 B of a row = 16 doubles; a
+// lane reads 16 B = 2 consecutive k and feeds element e to MFMA e, so MFMA (s, e) sums
+// k = 8s + 2q + e over the lane groups q (a permutation of the K-tile, the same for A and B). Staging
+// as dense_glds_kernel (global_load_lds_dwordx4, source-side XOR swizzle, two K-tile buffers).
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(512)
+dense_glds_f64_kernel(const double* __restrict__ A, const double* __restrict__ B, double* __restrict__ C,
+                      int64_t M, int N, int K, int64_t ldc, unsigned m_tiles, unsigned n_tiles) {
+    constexpr int BM = 256, BN = 128, KC = 8, KT = 16;
+    __shared__ uint4 lds[2 * (BM + BN) * KC];  // 2 x 48 KB
+    const unsigned bi = blockIdx.x, xcd = bi & 7u, j = bi >> 3;
+    const unsigned mt = (j / n_tiles) * 8u + xcd, nt = j % n_tiles;
+    if (mt >= m_tiles) return;  // uniform
+    const int64_t m0 = (int64_t)mt * BM;
+    const int n0 = (int)nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+    const int steps = K / KT;
+    const int srow = tid >> 3, sch = tid & 7, sxc = sch ^ (srow & 7);
+    const double* ga[4];
+    const double* gb[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ga[i] = A + std::min<int64_t>(m0 + i * 64 + srow, M - 1) * (int64_t)K + sxc * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) gb[i] = B + (int64_t)std::min(n0 + i * 64 + srow, N - 1) * K + sxc * 2;
+    auto stage = [&](int kt, int buf) {
+        uint4* base = lds + buf * (BM + BN) * KC;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds(ga[i] + (int64_t)kt * KT, base + i * 512 + 64 * w, 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds(gb[i] + (int64_t)kt * KT, base + BM * KC + i * 512 + 64 * w, 16, 0, 0);
+    };
+    f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int fr = lane & 15, fq = lane >> 4;
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < steps; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < steps) stage(kt + 1, cur ^ 1);
+        const uint4* sa = lds + cur * (BM + BN) * KC;
+        const uint4* sb = sa + BM * KC;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int cc = 4 * s + fq;
+            uint4 bfr[4];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int r = wn * 64 + ni * 16 + fr;
+                bfr[ni] = sb[r * KC + (cc ^ (r & 7))];
+            }
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int r = wm * 64 + mi * 16 + fr;
+                const uint4 afr = sa[r * KC + (cc ^ (r & 7))];
+                const double a0 = __hiloint2double((int)afr.y, (int)afr.x), a1 = __hiloint2double((int)afr.w, (int)afr.z);
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    const double b0 = __hiloint2double((int)bfr[ni].y, (int)bfr[ni].x);
+                    const double b1 = __hiloint2double((int)bfr[ni].w, (int)bfr[ni].z);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[mi][ni], 0, 0, 0);
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int c = n0 + wn * 64 + ni * 16 + fr;
+            if (c >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + wm * 64 + mi * 16 + fq + 4 * r;
+                if (row < M) C[row * ldc + c] = acc[mi][ni][r];
+            }
+        }
+}
+
+int launch_dense_f64(const void* X, const void* G, double* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
+                     hipStream_t st) {
+    const unsigned m_tiles = (unsigned)((n + 255) / 256), n_tiles = (unsigned)((p + 127) / 128);
+    const uint64_t blocks = (uint64_t)((m_tiles + 7) / 8) * 8ull * n_tiles;
+    if (blocks >= (1ull << 31)) return fail(RP_ERR_UNSUPPORTED, "too many rows for one launch");
+    hipLaunchKernelGGL(dense_glds_f64_kernel, dim3((unsigned)blocks), dim3(512), 0, st, (const double*)X,
+                       (const double*)G, Y, n, (int)p, (int)m, ldy, m_tiles, n_tiles);
+    HIP_TRY(hipGetLastError());
+    return RP_OK;
+}
+
 template <typename T, int WM, int WN, int TM, int TN, int STAGES, int DEPTH = 1>
 int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
                  hipStream_t st) {
@@ -386,11 +487,12 @@ extern "C" int rp_dense_set_variant(int32_t variant) {
 }
 
 extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype, int64_t n, int64_t m,
-                                       const void* G, int64_t p, float* Y, int64_t ldy, void* stream) {
+                                       const void* G, int64_t p, void* Y, int64_t ldy, void* stream) {
     if (!X || !G || !Y) return fail(RP_ERR_INVALID, "NULL operand");
-    if (dtype != RP_F32 && dtype != RP_BF16) return fail(RP_ERR_INVALID, "dtype must be RP_F32 or RP_BF16");
+    if (dtype != RP_F32 && dtype != RP_BF16 && dtype != RP_F64)
+        return fail(RP_ERR_INVALID, "dtype must be RP_F32, RP_BF16 or RP_F64");
     if (n < 0 || m <= 0 || p <= 0 || ldy < p) return fail(RP_ERR_INVALID, "bad shape");
-    const int step = dtype == RP_BF16 ? 64 : 32;
+    const int step = dtype == RP_BF16 ? 64 : dtype == RP_F32 ? 32 : 16;
     if (m % step) return fail(RP_ERR_UNSUPPORTED, "m=%lld must be a multiple of %d", (long long)m, step);
     if (m > INT32_MAX || p > INT32_MAX) return fail(RP_ERR_UNSUPPORTED, "m or p too large");
     const uintptr_t al = (uintptr_t)X | (uintptr_t)G;
@@ -400,6 +502,7 @@ extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype,
     const int sv = g_dense_variant.load(std::memory_order_relaxed);
     const int v = sv >= 0 ? sv : (dtype == RP_BF16 ? kDenseVariantBf16 : kDenseVariantF32);
     hipStream_t st = (hipStream_t)stream;
-    return dtype == RP_BF16 ? dispatch_dense<uint16_t>(v, X, G, Y, n, m, p, ldy, st)
-                            : dispatch_dense<float>(v, X, G, Y, n, m, p, ldy, st);
+    if (dtype == RP_F64) return launch_dense_f64(X, G, (double*)Y, n, m, p, ldy, st);
+    return dtype == RP_BF16 ? dispatch_dense<uint16_t>(v, X, G, (float*)Y, n, m, p, ldy, st)
+                            : dispatch_dense<float>(v, X, G, (float*)Y, n, m, p, ldy, st);
 }

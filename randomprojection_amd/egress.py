@@ -64,12 +64,44 @@ def rows(ids, labels, C):
         yield ids[i], labels[i], make_vector(C.shape[1], cj[s:e], cx[s:e])
 
 
+_MAX_LIST_ENTRIES = 2**31 - 1  # Arrow list<...> offsets are int32
+
+
+def _row_slices(indptr, limit=_MAX_LIST_ENTRIES):
+    """[r0, r1) row ranges whose entries each fit one Arrow list array (int32 offsets)."""
+    n, out, r0 = len(indptr) - 1, [], 0
+    while r0 < n or not out:
+        r1 = int(np.searchsorted(indptr, indptr[r0] + limit, side="right")) - 1
+        r1 = max(r1, r0 + 1) if n else 0
+        if r1 > n:
+            r1 = n
+        if r1 - r0 == 1 and indptr[r1] - indptr[r0] > limit:
+            raise ValueError("one row holds more than 2^31 - 1 entries")
+        out.append((r0, r1))
+        r0 = r1
+        if n == 0:
+            break
+    return out
+
+
 def _table(ids, labels, C):
+    """The partition as a pyarrow Table; a partition past 2^31 - 1 output entries becomes several
+    record batches (each with its own int32 list offsets), never a silently wrapped offset."""
     import pyarrow as pa
 
     C = _sorted_csr(C)
+    if C.nnz <= _MAX_LIST_ENTRIES:
+        return _table_part(ids, labels, C)
+    parts = [_table_part(ids[a:b], labels[a:b], C[a:b]) for a, b in _row_slices(np.asarray(C.indptr, np.int64))]
+    return pa.concat_tables(parts)
+
+
+def _table_part(ids, labels, C):
+    import pyarrow as pa
+
     n, p = C.shape
-    offs = pa.array(np.asarray(C.indptr, dtype=np.int32))
+    assert C.nnz <= _MAX_LIST_ENTRIES
+    offs = pa.array(np.asarray(C.indptr, dtype=np.int64) - int(C.indptr[0])).cast(pa.int32())
     it = pa.list_(pa.field("element", pa.int32(), nullable=False))
     vt = pa.list_(pa.field("element", pa.float64(), nullable=False))
     idx = pa.ListArray.from_arrays(offs, pa.array(C.indices.astype(np.int32, copy=False)), type=it)

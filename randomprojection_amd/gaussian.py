@@ -5,14 +5,16 @@ Reference semantics: sklearn ``GaussianRandomProjection`` — ``components_ = rn
 ``transform(X) = X @ components_.T`` (:569-612), a plain dense GEMM (n x m) . (m x p). The
 reference scripts never call it; BASELINE lists it as the dense-contraction config.
 
-This module streams X through the GPU in row chunks and runs librp's hand-written MFMA GEMM
+This module streams X through the GPU in row chunks and runs librp's hand-written MFMA GEMMs
 (csrc/rp_dense.hip, ``rp_dense_project_device``) in
-  * "fp32": f32 inputs, f32 MFMA (v_mfma_f32_32x32x2_f32 — exact f32 products; gfx950 has no xf32)
-    with f32 accumulation — matches numpy's sgemm within summation-order rounding (normwise 1e-5);
-  * "bf16": inputs rounded to bf16, f32 accumulation (v_mfma_f32_32x32x16_bf16; 2x less HBM, 16x
-    MFMA rate) — documented reduced-precision mode, checked against an fp64 product of the
-    bf16-rounded inputs.
-f64 input (sklearn computes in X's dtype) goes to torch's f64 matmul (library GEMM).
+  * "fp32": f32 inputs, f32 MFMA (exact f32 products; gfx950 has no xf32) with f32 accumulation —
+    matches numpy's sgemm within summation-order rounding (normwise 1e-5);
+  * "fp64": f64 inputs, v_mfma_f64_16x16x4_f64 with f64 accumulation (sklearn computes in X's dtype);
+  * "bf16": inputs rounded to bf16, f32 accumulation (2x less HBM, 16x the f32 MFMA rate) —
+    documented reduced-precision mode, checked against an fp64 product of the bf16-rounded inputs.
+The kernels are the product path for device-resident X too: bf16 measured 1221 TF against 1325 TF for
+hipBLASLt on the same 131072 x 16384 -> 1024 block (profiles/r03_dense_*); end to end the pass is
+PCIe-bound either way (X does not fit in HBM).
 ``components_`` is generated bit-identically to sklearn (``srp_matrix.gaussian_random_matrix``).
 """
 from __future__ import annotations
@@ -24,7 +26,7 @@ from sklearn.utils.validation import check_is_fitted, validate_data
 
 from .srp_matrix import gaussian_random_matrix
 
-__all__ = ["GaussianRandomProjection", "dense_project_device"]
+__all__ = ["GaussianRandomProjection", "dense_project_device", "prepare_operand"]
 
 
 def _torch():
@@ -35,59 +37,61 @@ def _torch():
     return torch
 
 
-def dense_project_device(X, C, out=None, compute: str = "fp32", stream=None):
-    """``X @ C.T`` for device tensors X (n x m) and C (p x m).
-    ``compute``: "fp32" (exact-f32 MFMA, f32 result) or "bf16" (bf16 inputs, f32 accumulate, f32
-    result) run librp's hand-written MFMA GEMM (rp_dense_project_device); "fp64" (f64 MFMA, f64
-    result) goes to torch's matmul."""
-    torch = _torch()
-    if compute in ("fp32", "bf16"):
-        import ctypes
+_STEP = {"bf16": 64, "fp32": 32, "fp64": 16}  # K multiple each kernel needs (zeros are padded)
 
-        from . import _native as nat
 
-        dt = torch.bfloat16 if compute == "bf16" else torch.float32
-        Xc = X.to(dt).contiguous()
-        Cc = C.to(dt).contiguous()
-        n, m = Xc.shape
-        p = Cc.shape[0]
-        if Cc.shape[1] != m:
-            raise ValueError(f"matmul: dimension mismatch {tuple(X.shape)} @ {tuple(C.shape)}.T")
-        y = out if out is not None else torch.empty(n, p, dtype=torch.float32, device=X.device)
-        if y.dtype != torch.float32 or y.shape != (n, p) or y.stride(1) != 1:
-            raise ValueError("out must be a float32 (n, p) tensor with unit column stride")
-        step = 64 if compute == "bf16" else 32
-        if m % step:  # pad the contraction (zeros add nothing)
-            padm = (m + step - 1) // step * step
-            Xc = torch.nn.functional.pad(Xc, (0, padm - m))
-            Cc = torch.nn.functional.pad(Cc, (0, padm - m))
-            m = padm
-        if stream is None:
-            stream = torch.cuda.current_stream(X.device).cuda_stream
-        nat.check(nat.load().rp_dense_project_device(
-            X.device.index or 0, ctypes.c_void_p(Xc.data_ptr()), nat.RP_BF16 if compute == "bf16" else nat.RP_F32,
-            n, m, ctypes.c_void_p(Cc.data_ptr()), p, ctypes.c_void_p(y.data_ptr()), y.stride(0),
-            ctypes.c_void_p(stream)))
-        return y
-    prev = torch.backends.cuda.matmul.allow_tf32
-    torch.backends.cuda.matmul.allow_tf32 = False  # never a reduced-precision f32 path
+def _dtype(torch, compute):
     try:
-        if compute == "bf16":
-            Xb = X if X.dtype == torch.bfloat16 else X.to(torch.bfloat16)
-            Cb = C if C.dtype == torch.bfloat16 else C.to(torch.bfloat16)
-            # aten::mm.dtype: bf16 operands, f32 accumulate, f32 result (never rounded to bf16)
-            y = torch.mm(Xb, Cb.t(), out_dtype=torch.float32)
-        elif compute == "fp32":
-            y = torch.matmul(X.float(), C.float().t())
-        elif compute == "fp64":
-            y = torch.matmul(X.double(), C.double().t())
-        else:
-            raise ValueError("compute must be 'fp32', 'fp64' or 'bf16'")
-    finally:
-        torch.backends.cuda.matmul.allow_tf32 = prev
-    if out is not None:
-        out.copy_(y)
-        return out
+        return {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[compute]
+    except KeyError:
+        raise ValueError("compute must be 'fp32', 'fp64' or 'bf16'") from None
+
+
+def prepare_operand(A, compute: str):
+    """A (rows x m) cast to the compute dtype, contiguous, the contraction padded with zeros to the
+    kernel's K multiple (zeros add nothing). Done once for the components in ``transform``."""
+    torch = _torch()
+    A = A.to(_dtype(torch, compute)).contiguous()
+    step = _STEP[compute]
+    if A.shape[1] % step:
+        A = torch.nn.functional.pad(A, (0, step - A.shape[1] % step))
+    return A
+
+
+def dense_project_device(X, C, out=None, compute: str = "fp32", stream=None, prepared_c: bool = False):
+    """``X @ C.T`` for device tensors X (n x m) and C (p x m) on librp's MFMA GEMM
+    (rp_dense_project_device): "fp32" (exact-f32 MFMA, f32 result), "bf16" (bf16 inputs, f32
+    accumulate, f32 result) or "fp64" (f64 MFMA, f64 result). ``prepared_c``: C already went through
+    ``prepare_operand`` for this compute mode. Runs on ``stream`` (default: torch's current stream);
+    temporaries made here are tied to that stream, so the caching allocator never hands them out
+    while the GEMM may still read them."""
+    import ctypes
+
+    from . import _native as nat
+
+    torch = _torch()
+    Cc = C if prepared_c else prepare_operand(C, compute)
+    n, m = X.shape
+    p = Cc.shape[0]
+    step = _STEP[compute]
+    if Cc.shape[1] != (m + step - 1) // step * step:
+        raise ValueError(f"matmul: dimension mismatch {tuple(X.shape)} @ {tuple(C.shape)}.T")
+    Xc = prepare_operand(X, compute)
+    ydt = torch.float64 if compute == "fp64" else torch.float32
+    y = out if out is not None else torch.empty(n, p, dtype=ydt, device=X.device)
+    if y.dtype != ydt or y.shape != (n, p) or y.stride(1) != 1:
+        raise ValueError(f"out must be a {ydt} (n, p) tensor with unit column stride")
+    cur = torch.cuda.current_stream(X.device)
+    if stream is None:
+        stream = cur.cuda_stream
+    elif stream != cur.cuda_stream:  # the GEMM reads Xc / Cc on another stream: keep them alive for it
+        ext = torch.cuda.ExternalStream(stream, device=X.device)
+        for t in (Xc, Cc):
+            t.record_stream(ext)
+    code = {"bf16": nat.RP_BF16, "fp32": nat.RP_F32, "fp64": nat.RP_F64}[compute]
+    nat.check(nat.load().rp_dense_project_device(
+        X.device.index or 0, ctypes.c_void_p(Xc.data_ptr()), code, n, Xc.shape[1], ctypes.c_void_p(Cc.data_ptr()), p,
+        ctypes.c_void_p(y.data_ptr()), y.stride(0), ctypes.c_void_p(stream)))
     return y
 
 
@@ -121,6 +125,7 @@ class GaussianRandomProjection(_SkGaussianRandomProjection):
         mode = self.compute if self.compute != "auto" else ("fp64" if X.dtype == np.float64 else "fp32")
         wdt = np.float64 if mode == "fp64" else np.float32
         C = torch.as_tensor(np.ascontiguousarray(self.components_, dtype=wdt), device=dev)
+        Cp = prepare_operand(C, mode)  # cast and padded once for every chunk
         n = X.shape[0]
         out = np.empty((n, C.shape[0]), dtype=wdt)
         for s in range(0, n, self.chunk_rows):
@@ -128,7 +133,7 @@ class GaussianRandomProjection(_SkGaussianRandomProjection):
             blk = X[s:e]
             blk = blk.toarray() if sp.issparse(blk) else blk
             xb = torch.as_tensor(np.ascontiguousarray(blk, dtype=wdt), device=dev)
-            out[s:e] = dense_project_device(xb, C, compute=mode).cpu().numpy()
+            out[s:e] = dense_project_device(xb, Cp, compute=mode, prepared_c=True).cpu().numpy()
         return out
 
     def __getstate__(self):

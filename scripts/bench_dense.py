@@ -22,12 +22,12 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-PEAK_TF = {"fp32": 157.3, "bf16": 2500.0}
+PEAK_TF = {"fp32": 157.3, "bf16": 2500.0, "fp64": 78.6}  # MI355X dense peaks (fp64 matrix = vector rate)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--compute", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--compute", choices=["fp32", "bf16", "fp64"], default="fp32")
     ap.add_argument("--chunk", type=int, default=131072)
     ap.add_argument("--m", type=int, default=16384)
     ap.add_argument("--p", type=int, default=1024)
@@ -50,12 +50,12 @@ def main():
 
     nat.check(nat.load().rp_dense_set_variant(args.variant))
     torch.cuda.set_device(0)
-    dt = torch.bfloat16 if args.compute == "bf16" else torch.float32
+    dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[args.compute]
     C = torch.as_tensor(gaussian_random_matrix(args.p, args.m, random_state=123).astype("float32"), device="cuda")
     C = C.to(dt)
     g = torch.Generator(device="cuda").manual_seed(5)
     X = torch.randn(args.chunk, args.m, device="cuda", generator=g).to(dt)
-    out = torch.empty(args.chunk, args.p, device="cuda", dtype=torch.float32)
+    out = torch.empty(args.chunk, args.p, device="cuda", dtype=torch.float64 if dt == torch.float64 else torch.float32)
     flop = 2.0 * args.chunk * args.m * args.p
 
     def torch_mm():

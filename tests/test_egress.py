@@ -45,3 +45,18 @@ def test_parquet_roundtrip_and_spark_schema(tmp_path):
     assert sch == json.loads(SPARK_SCHEMA_JSON)
     assert [f["name"] for f in sch["fields"]] == ["id", "label", "features"]
     assert sch["fields"][2]["type"]["class"] == "org.apache.spark.ml.linalg.VectorUDT"
+
+
+def test_row_slices_bound_list_offsets():
+    """Partitions past 2^31 - 1 entries are split into record batches whose int32 list offsets
+    cannot wrap (checked on the slicing rule with a small limit)."""
+    import numpy as np
+
+    from randomprojection_amd.egress import _row_slices
+
+    indptr = np.array([0, 3, 3, 9, 10, 20, 21], dtype=np.int64)
+    sl = _row_slices(indptr, limit=10)
+    assert sl[0][0] == 0 and sl[-1][1] == 6
+    assert all(a < b for a, b in sl) and all(sl[i][1] == sl[i + 1][0] for i in range(len(sl) - 1))
+    assert all(indptr[b] - indptr[a] <= 10 for a, b in sl)
+    assert _row_slices(np.array([0], dtype=np.int64)) == [(0, 0)]

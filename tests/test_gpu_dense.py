@@ -51,7 +51,7 @@ def test_sparse_input():
 
 
 @pytest.mark.parametrize("variant", [-1, 5, 10])
-@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("compute", ["fp32", "bf16", "fp64"])
 @pytest.mark.parametrize("shape", [(1, 64, 1), (300, 4096, 200), (1000, 16384, 1024), (257, 192, 129)])
 def test_mfma_kernel_ragged_shapes(compute, shape, variant):
     """librp's MFMA GEMM kernels (the default, the register-staged 256 x 256 tile and the LDS-direct
@@ -61,18 +61,22 @@ def test_mfma_kernel_ragged_shapes(compute, shape, variant):
     from randomprojection_amd import _native as nat
     from randomprojection_amd.gaussian import dense_project_device
 
+    if compute == "fp64" and variant != -1:
+        pytest.skip("one f64 kernel")
     nat.check(nat.load().rp_dense_set_variant(variant))
 
     n, m, p = shape
     rng = np.random.default_rng(n + m + p)
-    X = torch.as_tensor(rng.standard_normal((n, m)).astype(np.float32), device="cuda")
-    C = torch.as_tensor(rng.normal(0, 1 / 32, (p, m)).astype(np.float32), device="cuda")
+    wdt = np.float64 if compute == "fp64" else np.float32
+    X = torch.as_tensor(rng.standard_normal((n, m)).astype(wdt), device="cuda")
+    C = torch.as_tensor(rng.normal(0, 1 / 32, (p, m)).astype(wdt), device="cuda")
     Y = dense_project_device(X, C, compute=compute).cpu().numpy()
-    dt = torch.bfloat16 if compute == "bf16" else torch.float32
+    dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[compute]
     ref = X.to(dt).double().cpu().numpy() @ C.to(dt).double().cpu().numpy().T
-    assert Y.shape == (n, p) and Y.dtype == np.float32
-    assert _rel(Y, ref) < 1e-5  # north_star fp32 tolerance (K = 16384 f32 fma chains: ~2e-6 measured)
-    out = torch.full((n, p + 7), 7.0, device="cuda")[:, :p]  # a strided output view
+    assert Y.shape == (n, p) and Y.dtype == wdt
+    # north_star tolerances: fp32 1e-5 (K = 16384 f32 fma chains: ~2e-6 measured), fp64 1e-12
+    assert _rel(Y, ref) < (1e-12 if compute == "fp64" else 1e-5)
+    out = torch.full((n, p + 7), 7.0, device="cuda", dtype=torch.float64 if compute == "fp64" else torch.float32)[:, :p]
     dense_project_device(X, C, out=out, compute=compute)
     nat.check(nat.load().rp_dense_set_variant(-1))
     assert np.array_equal(out.cpu().numpy(), Y)
