@@ -146,6 +146,13 @@ def load(path: str = None):
     return lib
 
 
+def capacity_error(code: int, msg: str, nnz: int) -> RPError:
+    """RP_ERR_CAPACITY as an exception carrying the exact nnz the output needs."""
+    e = RPError(code, msg)
+    e.nnz = nnz
+    return e
+
+
 def check(rc: int):
     if rc != RP_OK:
         raise RPError(rc, load().rp_last_error().decode(errors="replace"))

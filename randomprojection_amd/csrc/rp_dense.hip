@@ -10,12 +10,12 @@
 //   f32:  exact f32 products (gfx950 has no xf32), f32 accumulate (v_mfma_f32_16x16x4_f32 / _32x32x2_f32).
 //
 // Two kernel families (rp_dense_set_variant picks one for measurements):
-//  * dense_glds_kernel (variant 10, the bf16 default): 256 x 256 tile, 8 waves of 128 x 64, 16 x 16
+//  * dense_glds_kernel (variant 10, the default): 256 x 256 tile, 8 waves of 128 x 64, 16 x 16
 //    MFMAs, operands staged global -> LDS by global_load_lds_dwordx4 (no VGPR round trip), XOR
 //    swizzle applied on the source address, two K-tile buffers with the next K-tile in flight during
 //    this one's MFMAs (description above the kernel);
-//  * dense_nt_kernel (variants 0-9; variant 5 = 256 x 256, 8 waves, 32 x 32 MFMAs, two LDS stages, is
-//    the f32 default): the next K step loaded global -> registers during the MFMAs, then written to
+//  * dense_nt_kernel (variants 0-9; variant 5 = 256 x 256, 8 waves, 32 x 32 MFMAs, two LDS stages, the
+//    round-2 default): the next K step loaded global -> registers during the MFMAs, then written to
 //    the other LDS buffer (one barrier per step); LDS rows of 128 B XOR-swizzled (chunk c of row r at
 //    c ^ (r & 7)); f32 permutes the K order inside a step so every lane reads 64 contiguous bytes.
 // Block -> tile map is XCD-aware in both: XCD x (workgroup i runs on XCD i % 8) takes the M tiles
@@ -455,9 +455,9 @@ int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, i
 // tile variants (RP_DENSE_VARIANT, measurements): 0 = 128x128 2 stages, 1 = 128x128 1 stage,
 // 2 = 256x128 1 stage, 3 = 128x256 2 stages (8 waves), 4 = 256x256 1 stage (8 waves), 5 = 256x256
 // 2 stages (128 KB LDS, 8 waves)
-// defaults per dtype: bf16 LDS-direct 256 x 256 (1221 TF vs 355 for variant 5, profiles/r03_dense_*),
-// f32 the register-staged 256 x 256 two-stage tile until the LDS-direct f32 form measures faster
-constexpr int kDenseVariantBf16 = 10, kDenseVariantF32 = 5;
+// defaults: the LDS-direct 256 x 256 kernel for both (measured, profiles/r03_dense_*: bf16 975-1221 TF
+// vs 353 for variant 5; f32 133 TF vs 97)
+constexpr int kDenseVariantBf16 = 10, kDenseVariantF32 = 10;
 template <typename T>
 int dispatch_dense(int v, const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
                    hipStream_t st) {

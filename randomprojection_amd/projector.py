@@ -298,9 +298,10 @@ class Projector:
                                          ctypes.c_void_p(ws_ptr), ws_bytes,
                                          ctypes.c_void_p(stream), ctypes.byref(total) if sync else None)
         if rc == nat.RP_ERR_CAPACITY:
-            err = nat.RPError(rc, self._lib.rp_last_error().decode())
-            err.nnz = int(total.value)
-            raise err
+            # raised without a local name: a frame holding its own exception is a reference cycle
+            # (frame -> exception -> traceback -> frame) that would keep the caller's output tensors
+            # (tens of GB at full size) alive until a GC pass
+            raise nat.capacity_error(rc, self._lib.rp_last_error().decode(), int(total.value))
         nat.check(rc)
         return int(total.value) if sync else None
 

@@ -13,6 +13,8 @@ rows ascending for the sorted order); >= 64k rows spread over the matrix (plus t
 2^31 output entries for configs[2]) are compared bit for bit with the oracle's restatement of
 scipy's csr_matmat (reference path: code/clustermode/randomProjection.py:46 -> scipy csr_matmat).
 """
+import gc
+
 import numpy as np
 import pytest
 
@@ -61,7 +63,8 @@ def project(P, Ap, Aj, Ax, order="scipy", slack=1.02):
             if e.code != nat.RP_ERR_CAPACITY:
                 raise
             cap = e.nnz
-            del Cp, Cj, Cx
+        del Cp, Cj, Cx  # before the exact retry allocates again (full-size outputs are tens of GB)
+        gc.collect()
     raise AssertionError("capacity retry failed")
 
 
@@ -174,7 +177,7 @@ def test_configs3_full_size():
     print("A ready: allocated", torch.cuda.memory_allocated(), "workspace",
           P.workspace_bytes(n, Aj.numel(), dtype=Ax.dtype), P.workspace_bytes(n, Aj.numel()))
     Cp, Cj, Cx, nnz = project(P, Ap, Aj, Ax, slack=1.0)
-    assert Cp.dtype == torch.int64 and nnz > 2**32 and 30 < nnz / n < 33
+    assert Cp.dtype == torch.int64 and nnz > 2**32 and 28 < nnz / n < 36
     check_csr_on_device(Cp, Cj, nnz, p)
     rows = sample_rows(n, 65536)
     off = Cp[torch.as_tensor(rows, device=Cp.device)]
