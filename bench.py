@@ -85,6 +85,8 @@ def step_kernels(plan, staged_run):
         if plan["staged"] == "auto":
             ks = ["lpr_choose_kernel"] + ks
         return ks
+    if plan["pipeline"] == "longrow":
+        return ["lrw_main_kernel", "lrw_heavy_kernel", "defer_copy_kernel"]
     ks = ["spgemm_lookback_kernel", "defer_copy_kernel"]
     return (["stage_partition_kernel", "stage_gather_kernel"] + ks) if plan["staged"] else ks
 
@@ -111,6 +113,8 @@ def main():
     ap.add_argument("--order", choices=["scipy", "sorted"], default="scipy")
     ap.add_argument("--staging", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--stage-shift", type=int, default=0, help="2^shift features per staging bucket (0 = auto)")
+    ap.add_argument("--pipeline", choices=["auto", "tile", "rowlane", "longrow"], default="auto",
+                    help="force a kernel pipeline where it can run (results identical; measurements)")
     ap.add_argument("--cpu-sample-rows", type=int, default=None)
     ap.add_argument("--cpu-part-rows", type=int, default=100_000,
                     help="rows per recipe partition (one per core) in the CPU baseline")
@@ -214,6 +218,8 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     if args.staging != "auto" or args.stage_shift:
         P.set_staging(args.staging, args.stage_shift)
+    if args.pipeline != "auto":
+        P.set_option("pipeline", args.pipeline)
     try:  # full workspace (deferred tile output + staging); the minimal one if HBM is short
         ws = torch.empty(P.workspace_bytes(args.rows, nnz_a, dtype=Ax.dtype), dtype=torch.uint8, device=dev)
     except torch.OutOfMemoryError:
