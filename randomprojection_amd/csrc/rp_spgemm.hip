@@ -1215,8 +1215,9 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
 // (configs[3]: 100 entries, ~32 products per row). Every wave is its own tile of `rpt` consecutive
 // rows, taken in dispatch order from the tile counter, and runs scipy's csr_matmat on each row with
 // no block barrier:
-//   * the row's entries in rounds of 64 lanes (A and W loads of all rounds issued together), the
-//     products in (jj, kk) order into a wave buffer, sequence number q = buffer position;
+//   * the tile's entries as ONE flat stream in rounds of 64 lanes (A and W loads of 8 rounds in
+//     flight together), products in (row, jj, kk) order into a wave buffer; a row-start bitmap gives
+//     each row's first product; sequence number q = position within the row;
 //   * first touch per column by ONE LDS atomicMax per product on a direct-mapped table of p words
 //     (key = row tag << 16 | 0xffff - q: among the current row's keys the largest is the smallest
 //     q; older rows' keys are smaller, so nothing is cleared between rows): a product leads iff the
@@ -1224,29 +1225,30 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
 //   * a leader's sum starts at +0 + its product; the (rare) later products of its column are added
 //     in sequence order by one lane; kept = sum != 0 (NaN kept, +-0 dropped); scipy's order =
 //     descending leader q (reverse first touch), or ascending column (a p-bit map, popcounts);
-//   * the tile's entries are staged in LDS, then placed with the wave-level decoupled look-back,
+//   * the kept entries are compacted to the front of the product buffer (a row's outputs never pass
+//     its own first product), then placed with the wave-level decoupled look-back,
 //     or parked in the deferred pool exactly as the tile pipeline does (defer_copy_kernel).
-// A tile past the wave's caps (a row of more than kLrwPCap products or 64 x kLrwRounds entries, more
-// than kLrwOCap outputs) or finding the pool full is flagged and done by lrw_heavy_kernel (the exact
+// A tile past the wave's caps (more than 64 x kLrwERounds entries or kLrwTCap products, a row of more
+// than kLrwPCap products) or finding the pool full is flagged and done by lrw_heavy_kernel (the exact
 // dense accumulator, tiles in order) before defer_copy_kernel; no wave ever waits unboundedly.
 constexpr int kLrwPCap = 256;     // products of one row on the fast path
-constexpr int kLrwRounds = 4;     // entries of one row on the fast path: kLrwRounds x 64
-constexpr int kLrwOCap = 512;     // outputs of one wave tile staged in LDS
+constexpr int kLrwTCap = 512;     // products of one wave tile (LDS buffer; the tile's output is compacted into it)
+constexpr int kLrwChunk = 8;      // entry rounds (x 64) whose loads are in flight together
+constexpr int kLrwERounds = 16;   // entries of one wave tile on the fast path: 16 x 64
 constexpr int kLrwPMax = 2048;    // columns of R (first-touch table 4 B per column, bitmap p bits)
 constexpr int kLrwRowsMax = 64;   // rows per wave tile
 
 struct LrwLayout {
-    size_t tab, bm, pc, pv, oc, ov, ro, total;
+    size_t tab, bm, rs, ps, pc, pv, total;
     __host__ __device__ LrwLayout(int p, size_t vs) {
         auto al = [](size_t v) { return (v + 15) & ~size_t(15); };
         tab = 0;
         bm = al(4 * (size_t)p);
-        pc = bm + al(4 * (size_t)((p + 31) / 32));
-        pv = pc + al(2 * (size_t)kLrwPCap);
-        oc = pv + al(vs * (size_t)kLrwPCap);
-        ov = oc + al(2 * (size_t)kLrwOCap);
-        ro = ov + al(vs * (size_t)kLrwOCap);
-        total = ro + al(2 * (size_t)(kLrwRowsMax + 1));
+        rs = bm + al(4 * (size_t)((p + 31) / 32));
+        ps = rs + al(8 * (size_t)kLrwERounds);
+        pc = ps + al(2 * (size_t)(kLrwRowsMax + 1));
+        pv = pc + al(2 * (size_t)kLrwTCap);
+        total = pv + al(vs * (size_t)kLrwTCap);
     }
 };
 
@@ -1256,7 +1258,7 @@ __device__ __forceinline__ T lane_value(T v, int l) {
 }
 
 template <typename T, typename IP, typename OP, typename OI>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
 lrw_main_kernel(PackedR R, T mag, int p, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
                 const T* __restrict__ Ax, OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
                 unsigned long long capacity, int rpt, int order, Workspace* ws, unsigned n_tiles,
@@ -1265,11 +1267,10 @@ lrw_main_kernel(PackedR R, T mag, int p, int64_t n_rows, const IP* __restrict__ 
     const LrwLayout L(p, sizeof(T));
     uint32_t* tab = reinterpret_cast<uint32_t*>(lds + L.tab);
     uint32_t* bm = reinterpret_cast<uint32_t*>(lds + L.bm);
+    uint64_t* rsb = reinterpret_cast<uint64_t*>(lds + L.rs);   // row-start bitmap over the tile's entries
+    uint16_t* ps = reinterpret_cast<uint16_t*>(lds + L.ps);    // row -> first product; ps[nrows] = total
     uint16_t* pcol = reinterpret_cast<uint16_t*>(lds + L.pc);
     T* pval = reinterpret_cast<T*>(lds + L.pv);
-    uint16_t* ocol = reinterpret_cast<uint16_t*>(lds + L.oc);
-    T* oval = reinterpret_cast<T*>(lds + L.ov);
-    uint16_t* ro = reinterpret_cast<uint16_t*>(lds + L.ro);
     unsigned long long* states = reinterpret_cast<unsigned long long*>(ws + 1);
     const int lane = threadIdx.x;
     const int nbw = (p + 31) >> 5;
@@ -1279,216 +1280,244 @@ lrw_main_kernel(PackedR R, T mag, int p, int64_t n_rows, const IP* __restrict__ 
     while (true) {
         unsigned tile = 0;
         if (lane == 0) tile = atomicAdd(&ws->tile_counter, 1u);
-        tile = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)__shfl((int)tile, 0, 64));
+        tile = (unsigned)__builtin_amdgcn_readfirstlane(__shfl((int)tile, 0, 64));
         if (tile >= n_tiles) break;  // uniform
         const int64_t row0 = (int64_t)tile * rpt;
         const int nrows = (int)std::min<int64_t>(rpt, n_rows - row0);
-        uint32_t obase = 0;
-        bool heavy = false;
-        for (int i = 0; i < nrows; ++i) {
-            if (++tag == 0x10000u) {  // tag space used up: clear the table (every ~65K rows of a wave)
-                __builtin_amdgcn_wave_barrier();
-                for (int c = lane; c < p; c += 64) tab[c] = 0u;
-                tag = 1;
-                __builtin_amdgcn_wave_barrier();
-            }
-            const int64_t a0 = (int64_t)Ap[row0 + i], a1 = (int64_t)Ap[row0 + i + 1];
-            const int64_t len = a1 - a0;
-            if (len > 64 * kLrwRounds) {
-                heavy = true;
-                break;
-            }
-            ro[i] = (uint16_t)obase;
-            const int nr = (int)((len + 63) >> 6);
-            // ---- the row's entries: A and W words of every round in flight together
-            int32_t jr[kLrwRounds];
-            T xr[kLrwRounds];
-            uint64_t wr[kLrwRounds];
-#pragma unroll
-            for (int u = 0; u < kLrwRounds; ++u) {
-                if (u < nr) {
-                    const int64_t e = std::min<int64_t>(a0 + 64 * u + lane, a1 - 1);
-                    jr[u] = Aj[e];
-                    xr[u] = Ax[e];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kLrwRounds; ++u)
-                if (u < nr) wr[u] = R.W[jr[u]];
-            uint32_t P = 0;
-#pragma unroll
-            for (int u = 0; u < kLrwRounds; ++u) {
-                if (u >= nr) break;
-                const bool ve = 64 * u + lane < len;
-                const uint32_t n = (uint32_t)(wr[u] >> 61);
-                uint64_t d = wr[u];
-                uint32_t cnt = n;
-                if (n == 7) {  // more than 4 entries: the record in O (rare)
-                    const uint64_t rec = wr[u] & kLow61;
-                    cnt = R.O[rec];
-                    d = kOvf | (rec + 1);
-                }
-                cnt = ve ? cnt : 0u;
-                const uint32_t inc = wave_scan_dpp(cnt);
-                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-                if (P + tot > (uint32_t)kLrwPCap) {  // uniform
-                    P = ~0u;
-                    break;
-                }
-                const uint32_t q0 = P + inc - cnt;
-                for (uint32_t t = 0; t < cnt; ++t) {
-                    uint32_t col;
-                    T v;
-                    r_product<T>(R, mag, d, t, xr[u], col, v);
-                    pcol[q0 + t] = (uint16_t)col;
-                    pval[q0 + t] = v;
-                }
-                P += tot;
-            }
-            if (P == ~0u) {
-                heavy = true;
-                break;
+        // ---- the tile's entries [A0, A1) as one flat stream; row starts into a bitmap
+        const int64_t A0 = (int64_t)Ap[row0], A1 = (int64_t)Ap[row0 + nrows];
+        const int64_t ne = A1 - A0;
+        bool heavy = ne > 64 * kLrwERounds;
+        if (!heavy) {
+            for (int k = lane; k < kLrwERounds; k += 64) rsb[k] = 0ull;
+            __builtin_amdgcn_wave_barrier();
+            bool rnz = false;  // this lane's row (lane < nrows) has entries
+            if (lane < nrows) {
+                const int64_t s = (int64_t)Ap[row0 + lane] - A0;
+                const int64_t e = (int64_t)Ap[row0 + lane + 1] - A0;
+                rnz = e > s;
+                if (rnz) atomicOr(reinterpret_cast<unsigned long long*>(&rsb[s >> 6]), 1ull << (s & 63));
             }
             __builtin_amdgcn_wave_barrier();
-            // ---- first touch, leaders' sums (sequence order), kept flags
-            const int np = (int)((P + 63) >> 6);
-            uint64_t lead[kLrwPCap / 64];
-            uint32_t lq[kLrwPCap / 64];
+            // ---- products of every entry in (row, jj, kk) order = flat entry order; the
+            // product offset of each row's first entry goes to ps[row]
+            const int nr = (int)((ne + 63) >> 6);
+            uint32_t P = 0, rows_seen = 0;
+            const T* __restrict__ Axt = Ax + A0;
+            const int32_t* __restrict__ Ajt = Aj + A0;
+            for (int c0 = 0; c0 < nr && !heavy; c0 += kLrwChunk) {
+                int32_t jr[kLrwChunk];
+                T xr[kLrwChunk];
+                uint64_t wr[kLrwChunk];
 #pragma unroll
-            for (int v = 0; v < kLrwPCap / 64; ++v) {
-                lead[v] = 0;
-                lq[v] = 0;
-                if (v >= np) continue;
-                const uint32_t q = 64u * v + lane;
-                const bool vq = q < P;
-                const uint32_t c = vq ? pcol[q] : 0u;
-                const T val = vq ? pval[q] : T(0);
-                const uint32_t key = (tag << 16) | (0xffffu - q);
-                if (vq) atomicMax(&tab[c], key);
+                for (int u = 0; u < kLrwChunk; ++u) {
+                    if (c0 + u < nr) {
+                        const int64_t e = std::min<int64_t>(64 * (c0 + u) + lane, ne - 1);
+                        jr[u] = Ajt[e];
+                        xr[u] = Axt[e];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kLrwChunk; ++u)
+                    if (c0 + u < nr) wr[u] = R.W[jr[u]];
+#pragma unroll
+                for (int u = 0; u < kLrwChunk; ++u) {
+                    if (c0 + u >= nr) break;
+                    const int k = c0 + u;
+                    const bool ve = 64 * k + lane < ne;
+                    const uint32_t n = (uint32_t)(wr[u] >> 61);
+                    uint64_t d = wr[u];
+                    uint32_t cnt = n;
+                    if (n == 7) {  // more than 4 entries: the record in O (rare)
+                        const uint64_t rec = wr[u] & kLow61;
+                        cnt = R.O[rec];
+                        d = kOvf | (rec + 1);
+                    }
+                    cnt = ve ? cnt : 0u;
+                    const uint32_t inc = wave_scan_dpp(cnt);
+                    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+                    if (P + tot > (uint32_t)kLrwTCap) {  // uniform
+                        heavy = true;
+                        break;
+                    }
+                    const uint32_t q0 = P + inc - cnt;
+                    const uint64_t fw = rsb[k];
+                    if (ve && ((fw >> lane) & 1ull)) {  // a row's first entry: its row index, its start
+                        const uint32_t rr = rows_seen + (uint32_t)__popcll(fw & ((1ull << lane) - 1ull));
+                        ps[rr] = (uint16_t)q0;
+                    }
+                    rows_seen += (uint32_t)__popcll(fw);
+                    for (uint32_t t = 0; t < cnt; ++t) {
+                        uint32_t col;
+                        T v;
+                        r_product<T>(R, mag, d, t, xr[u], col, v);
+                        pcol[q0 + t] = (uint16_t)col;
+                        pval[q0 + t] = v;
+                    }
+                    P += tot;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            // ps[k] holds the start of the k-th NONEMPTY row: spread the starts over all rows, an
+            // empty row starting where the next nonempty row starts (or at P)
+            if (!heavy) {
+                const uint64_t nz = __ballot(rnz);
+                uint32_t mine = P;
+                if (rnz) mine = ps[(uint32_t)__popcll(nz & ((1ull << lane) - 1ull))];
                 __builtin_amdgcn_wave_barrier();
-                const uint32_t first = vq ? tab[c] : 0u;
-                const bool isl = vq && first == key;
-                lead[v] = __ballot(isl);
-                if (isl) pval[q] = tadd<T>(T(0), val);
-                lq[v] = 0xffffu - (first & 0xffffu);  // the leader of this product's column
-                uint64_t nl = __ballot(vq && !isl);
+                const uint64_t after = nz & ~((2ull << lane) - 1ull);
+                const int nx = after ? __builtin_ctzll(after) : 64;
+                const uint32_t nxt = (uint32_t)__shfl((int)mine, nx & 63, 64);
+                const uint32_t start = rnz ? mine : (nx < 64 ? nxt : P);
+                if (lane <= nrows) ps[lane] = (uint16_t)(lane < nrows ? start : P);
                 __builtin_amdgcn_wave_barrier();
-                while (nl) {  // rare: products of an already-touched column, in sequence order
-                    const int l = __builtin_ctzll(nl);
-                    nl &= nl - 1;
-                    const uint32_t Lq = (uint32_t)__builtin_amdgcn_readlane((int)lq[v], l);
-                    const T lv = lane_value<T>(val, l);
-                    if (lane == 0) pval[Lq] = tadd<T>(pval[Lq], lv);
+            }
+            // ---- per row: first touch, leaders' sums in sequence order, kept entries compacted
+            // to the front of the product buffer in the row's output order
+            uint32_t obase = 0;
+            for (int i = 0; i < nrows && !heavy; ++i) {
+                if (++tag == 0x10000u) {  // tag space used up: clear the table (every ~65K rows of a wave)
+                    __builtin_amdgcn_wave_barrier();
+                    for (int c = lane; c < p; c += 64) tab[c] = 0u;
+                    tag = 1;
                     __builtin_amdgcn_wave_barrier();
                 }
-            }
-            uint64_t keep[kLrwPCap / 64];
-            uint32_t K = 0;
-#pragma unroll
-            for (int v = 0; v < kLrwPCap / 64; ++v) {
-                keep[v] = 0;
-                if (v >= np) continue;
-                const uint32_t q = 64u * v + lane;
-                const bool isl = (lead[v] >> lane) & 1ull;
-                keep[v] = __ballot(isl && pval[q] != T(0));
-                K += (uint32_t)__popcll(keep[v]);
-            }
-            if (obase + K > (uint32_t)kLrwOCap) {  // uniform
-                heavy = true;
-                break;
-            }
-            // ---- output positions: descending q (scipy) or ascending column (sorted)
-            if (order == RP_ORDER_SORTED) {
+                const uint32_t r0 = ps[i], r1 = ps[i + 1];
+                const uint32_t Pr = r1 - r0;
+                if (Pr > (uint32_t)kLrwPCap) {  // uniform
+                    heavy = true;
+                    break;
+                }
+                const int np = (int)((Pr + 63) >> 6);
+                uint64_t lead[kLrwPCap / 64];
+                uint32_t cq[kLrwPCap / 64];
 #pragma unroll
                 for (int v = 0; v < kLrwPCap / 64; ++v) {
+                    lead[v] = 0;
+                    cq[v] = 0;
                     if (v >= np) continue;
-                    if ((keep[v] >> lane) & 1ull) {
-                        const uint32_t c = pcol[64u * v + lane];
-                        atomicOr(&bm[c >> 5], 1u << (c & 31));
+                    const uint32_t q = 64u * v + lane;
+                    const bool vq = q < Pr;
+                    const uint32_t c = vq ? pcol[r0 + q] : 0u;
+                    const T val = vq ? pval[r0 + q] : T(0);
+                    cq[v] = c;
+                    const uint32_t key = (tag << 16) | (0xffffu - q);
+                    if (vq) atomicMax(&tab[c], key);
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t first = vq ? tab[c] : 0u;
+                    const bool isl = vq && first == key;
+                    lead[v] = __ballot(isl);
+                    if (isl) pval[r0 + q] = tadd<T>(T(0), val);
+                    const uint32_t lq = 0xffffu - (first & 0xffffu);  // the leader of this product's column
+                    uint64_t nl = __ballot(vq && !isl);
+                    __builtin_amdgcn_wave_barrier();
+                    while (nl) {  // rare: products of an already-touched column, in sequence order
+                        const int l = __builtin_ctzll(nl);
+                        nl &= nl - 1;
+                        const uint32_t Lq = (uint32_t)__builtin_amdgcn_readlane((int)lq, l);
+                        const T lv = lane_value<T>(val, l);
+                        if (lane == 0) pval[r0 + Lq] = tadd<T>(pval[r0 + Lq], lv);
+                        __builtin_amdgcn_wave_barrier();
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
-                // word popcounts, exclusive prefix over the p bits (<= 64 words)
-                const uint32_t wbits = lane < nbw ? bm[lane] : 0u;
-                const uint32_t wc = (uint32_t)__popc(wbits);
-                const uint32_t wpre = wave_scan_dpp(wc) - wc;
+                uint64_t keep[kLrwPCap / 64];
+                T kv[kLrwPCap / 64];
+                uint32_t K = 0;
 #pragma unroll
                 for (int v = 0; v < kLrwPCap / 64; ++v) {
+                    keep[v] = 0;
+                    kv[v] = T(0);
                     if (v >= np) continue;
-                    const uint32_t q = 64u * v + lane;
-                    const bool kq = (keep[v] >> lane) & 1ull;
-                    const uint32_t c = kq ? pcol[q] : 0u;
-                    const uint32_t pw = (uint32_t)__shfl((int)wpre, (int)(c >> 5), 64);
-                    const uint32_t word = (uint32_t)__shfl((int)wbits, (int)(c >> 5), 64);
-                    if (kq) {
-                        const uint32_t pos = pw + (uint32_t)__popc(word & ((1u << (c & 31)) - 1u));
-                        ocol[obase + pos] = (uint16_t)c;
-                        oval[obase + pos] = pval[q];
-                    }
+                    const bool isl = (lead[v] >> lane) & 1ull;
+                    kv[v] = isl ? pval[r0 + 64u * v + lane] : T(0);
+                    keep[v] = __ballot(isl && kv[v] != T(0));
+                    K += (uint32_t)__popcll(keep[v]);
                 }
-                __builtin_amdgcn_wave_barrier();
-                if (lane < nbw) bm[lane] = 0u;
-            } else {
-                uint32_t after = 0;  // kept entries in later rounds
+                __builtin_amdgcn_wave_barrier();  // every read of the row's slots is done: compact
+                if (order == RP_ORDER_SORTED) {
 #pragma unroll
-                for (int v = kLrwPCap / 64 - 1; v >= 0; --v) {
-                    if (v >= np) continue;
-                    const uint32_t q = 64u * v + lane;
-                    const uint64_t above = lane == 63 ? 0ull : keep[v] >> (lane + 1);
-                    if ((keep[v] >> lane) & 1ull) {
-                        const uint32_t pos = after + (uint32_t)__popcll(above);
-                        ocol[obase + pos] = pcol[q];
-                        oval[obase + pos] = pval[q];
+                    for (int v = 0; v < kLrwPCap / 64; ++v)
+                        if (v < np && ((keep[v] >> lane) & 1ull)) atomicOr(&bm[cq[v] >> 5], 1u << (cq[v] & 31));
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t wbits = lane < nbw ? bm[lane] : 0u;
+                    const uint32_t wc = (uint32_t)__popc(wbits);
+                    const uint32_t wpre = wave_scan_dpp(wc) - wc;
+#pragma unroll
+                    for (int v = 0; v < kLrwPCap / 64; ++v) {
+                        if (v >= np) continue;
+                        const bool kq = (keep[v] >> lane) & 1ull;
+                        const uint32_t c = cq[v];
+                        const uint32_t pw = (uint32_t)__shfl((int)wpre, (int)(c >> 5), 64);
+                        const uint32_t word = (uint32_t)__shfl((int)wbits, (int)(c >> 5), 64);
+                        if (kq) {
+                            const uint32_t pos = pw + (uint32_t)__popc(word & ((1u << (c & 31)) - 1u));
+                            pcol[obase + pos] = (uint16_t)c;
+                            pval[obase + pos] = kv[v];
+                        }
                     }
-                    after += (uint32_t)__popcll(keep[v]);
-                }
-            }
-            obase += K;
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (heavy) {  // uniform: lrw_heavy_kernel does this tile (nothing published here)
-            if (lane == 0) tflag[tile] = 1;
-            __builtin_amdgcn_wave_barrier();
-            continue;
-        }
-        ro[nrows] = (uint16_t)obase;
-        __builtin_amdgcn_wave_barrier();
-        const unsigned long long g = lookback_wave(states, tile, obase, ws, defer_polls, true, defer_ticks);
-        if (g == ~0ull) {  // no prefix within the budget: park in the pool (or leave it to the heavy kernel)
-            unsigned long long o = 0;
-            if (lane == 0) {
-                o = atomicAdd(&ws->pool_used, (unsigned long long)obase);
-                if (o + obase <= dfr.pool_cap) {
-                    dfr.pofs[tile] = o;
-                    dfr.list[atomicAdd(&ws->n_deferred, 1u)] = tile;
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane < nbw) bm[lane] = 0u;
                 } else {
-                    o = ~0ull;
-                    tflag[tile] = 2;  // aggregate already published
+                    uint32_t after = 0;  // kept entries in later rounds
+#pragma unroll
+                    for (int v = kLrwPCap / 64 - 1; v >= 0; --v) {
+                        if (v >= np) continue;
+                        const uint64_t above = lane == 63 ? 0ull : keep[v] >> (lane + 1);
+                        if ((keep[v] >> lane) & 1ull) {
+                            const uint32_t pos = after + (uint32_t)__popcll(above);
+                            pcol[obase + pos] = (uint16_t)cq[v];
+                            pval[obase + pos] = kv[v];
+                        }
+                        after += (uint32_t)__popcll(keep[v]);
+                    }
                 }
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) ps[i] = (uint16_t)obase;  // now the row's output offset in the tile
+                obase += K;
+                __builtin_amdgcn_wave_barrier();
             }
-            o = __shfl(o, 0, 64);
-            if (o != ~0ull) {
-                uint16_t* hd = dfr.hdr + (size_t)tile * (rpt + 1);
-                for (int r = lane; r <= nrows; r += 64) hd[r] = ro[r];
-                uint16_t* __restrict__ pc = dfr.cols + o;
-                T* __restrict__ pv = reinterpret_cast<T*>(dfr.vals) + o;
-                for (uint32_t q = lane; q < obase; q += 64) {
-                    pc[q] = ocol[q];
-                    pv[q] = oval[q];
+            if (!heavy) {
+                if (lane == 0) ps[nrows] = (uint16_t)obase;
+                __builtin_amdgcn_wave_barrier();
+                const unsigned long long g = lookback_wave(states, tile, obase, ws, defer_polls, true, defer_ticks);
+                if (g == ~0ull) {  // no prefix within the budget: park in the pool (or leave it to the heavy kernel)
+                    unsigned long long o = 0;
+                    if (lane == 0) {
+                        o = atomicAdd(&ws->pool_used, (unsigned long long)obase);
+                        if (o + obase <= dfr.pool_cap) {
+                            dfr.pofs[tile] = o;
+                            dfr.list[atomicAdd(&ws->n_deferred, 1u)] = tile;
+                        } else {
+                            o = ~0ull;
+                            tflag[tile] = 2;  // aggregate already published
+                        }
+                    }
+                    o = __shfl(o, 0, 64);
+                    if (o != ~0ull) {
+                        uint16_t* hd = dfr.hdr + (size_t)tile * (rpt + 1);
+                        for (int r = lane; r <= nrows; r += 64) hd[r] = ps[r];
+                        uint16_t* __restrict__ pc = dfr.cols + o;
+                        T* __restrict__ pv = reinterpret_cast<T*>(dfr.vals) + o;
+                        for (uint32_t q = lane; q < obase; q += 64) {
+                            pc[q] = pcol[q];
+                            pv[q] = pval[q];
+                        }
+                    }
+                } else {
+                    for (int r = lane; r < nrows; r += 64) Cp[row0 + r] = (OP)(g + ps[r]);
+                    if (g + obase <= capacity)
+                        for (uint32_t q = lane; q < obase; q += 64) {
+                            Cj[g + q] = (OI)pcol[q];
+                            Cx[g + q] = pval[q];
+                        }
+                    if (tile == n_tiles - 1 && lane == 0) {
+                        Cp[n_rows] = (OP)(g + obase);
+                        ws->total = g + obase;
+                    }
                 }
-            }
-        } else {
-            for (int r = lane; r < nrows; r += 64) Cp[row0 + r] = (OP)(g + ro[r]);
-            if (g + obase <= capacity)
-                for (uint32_t q = lane; q < obase; q += 64) {
-                    Cj[g + q] = (OI)ocol[q];
-                    Cx[g + q] = oval[q];
-                }
-            if (tile == n_tiles - 1 && lane == 0) {
-                Cp[n_rows] = (OP)(g + obase);
-                ws->total = g + obase;
             }
         }
+        if (heavy && lane == 0) tflag[tile] = 1;  // lrw_heavy_kernel does this tile (nothing published here)
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -2940,7 +2969,7 @@ bool lrw_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
     if (h->layout != RP_LAYOUT_PACKED || h->p > kLrwPMax || n_rows <= 0 || nnz_a < 0) return false;
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
     const double avg = (double)nnz_a / (double)n_rows;
-    const bool fits = avg <= 64.0 * kLrwRounds * 0.75 && avg * ppe <= kLrwPCap / 2.0;
+    const bool fits = avg <= 640.0 && avg * ppe <= kLrwPCap / 2.0;
     if (h->opt_pipeline == 1 || h->opt_pipeline == 2) return false;  // tile / row-lane forced
     if (h->opt_pipeline == 3) return fits;                             // long-row wave forced
     return fits && avg >= kLrwMinRow;
@@ -2952,10 +2981,13 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
     auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
     if (!lpr_wanted(h, n_rows, nnz_a) && lrw_wanted(h, n_rows, nnz_a) && allow_defer) {
-        // one wave per tile of rpt rows, ~256 expected outputs per tile (the LDS stage holds 512)
+        // one wave per tile of rpt rows: <= 256 expected products (the buffer holds kLrwTCap = 512)
+        // and <= 640 expected entries (kLrwERounds x 64 = 1024 on the fast path)
         pl.lrw = true;
-        const double prow = std::max(1.0, (double)nnz_a / (double)n_rows * ppe);
-        pl.caps.rpt = (int)std::max(1.0, std::min((double)kLrwRowsMax, std::floor(256.0 / prow)));
+        const double arow = std::max(1.0, (double)nnz_a / (double)n_rows);
+        const double prow = std::max(1.0, arow * ppe);
+        pl.caps.rpt = (int)std::max(1.0, std::min({(double)kLrwRowsMax, std::floor(256.0 / prow),
+                                                   std::floor(640.0 / arow)}));
         pl.caps.cap_a = 0;
         pl.caps.cap_p = 0;
         pl.n_tiles = (n_rows + pl.caps.rpt - 1) / pl.caps.rpt;
@@ -3271,10 +3303,10 @@ int launch_lrw(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, con
     const size_t lds = LrwLayout(p, sizeof(T)).total;
     const void* fn = (const void*)lrw_main_kernel<T, IP, OP, OI>;
     HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, lds) != hipSuccess || per_cu < 1) per_cu = 1;
+    // persistent waves: as many as a CU can hold (32 waves; a wave that finds no tile exits at once)
+    int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) cus = 256;
-    const unsigned grid = (unsigned)std::min<int64_t>((int64_t)per_cu * cus, (int64_t)n_tiles);
+    const unsigned grid = (unsigned)std::min<int64_t>((int64_t)32 * cus, (int64_t)n_tiles);
     hipLaunchKernelGGL((lrw_main_kernel<T, IP, OP, OI>), dim3(grid), dim3(64), lds, st, R, mag, p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr, (OI*)c->indices,
                        (T*)c->data, (unsigned long long)c->capacity, pl.caps.rpt, order, ws, n_tiles, tflag, dfr,
