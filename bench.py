@@ -85,8 +85,6 @@ def step_kernels(plan, staged_run):
         if plan["staged"] == "auto":
             ks = ["lpr_choose_kernel"] + ks
         return ks
-    if plan["pipeline"] == "longrow":
-        return ["lrw_main_kernel", "lrw_heavy_kernel", "defer_copy_kernel"]
     ks = ["spgemm_lookback_kernel", "defer_copy_kernel"]
     return (["stage_partition_kernel", "stage_gather_kernel"] + ks) if plan["staged"] else ks
 
@@ -113,7 +111,7 @@ def main():
     ap.add_argument("--order", choices=["scipy", "sorted"], default="scipy")
     ap.add_argument("--staging", choices=["auto", "on", "off"], default="auto")
     ap.add_argument("--stage-shift", type=int, default=0, help="2^shift features per staging bucket (0 = auto)")
-    ap.add_argument("--pipeline", choices=["auto", "tile", "rowlane", "longrow"], default="auto",
+    ap.add_argument("--pipeline", choices=["auto", "tile", "rowlane"], default="auto",
                     help="force a kernel pipeline where it can run (results identical; measurements)")
     ap.add_argument("--cpu-sample-rows", type=int, default=None)
     ap.add_argument("--cpu-part-rows", type=int, default=100_000,

@@ -163,8 +163,7 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
 /* Per-projector tuning and test options (the library reads no environment variables). Results are
  * identical under every setting; only the schedule changes. value < default sentinel restores the
  * default.
- *   RP_OPT_PIPELINE      0 auto (default); 1 tile pipeline; 2 row-lane pipeline / 3 long-row wave
- *                        pipeline where it can run
+ *   RP_OPT_PIPELINE      0 auto (default); 1 tile pipeline; 2 row-lane pipeline where it can run
  *   RP_OPT_DEFER_POLLS   tile pipeline: -2 default (time budget); -1 tiles never park their output;
  *                        n >= 0 park after n unsuccessful look-back polls (time budget off)
  *   RP_OPT_DEFER_TICKS   256-row tiles' look-back wait budget in s_memrealtime ticks (100 MHz):
@@ -184,13 +183,12 @@ int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value);
 int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* value);
 
 /* The kernel pipeline rp_project_device would run for n_rows rows holding nnz_a entries with the
- * full workspace: *pipeline = RP_PIPE_TILE (tile SpGEMM with look-back), RP_PIPE_ROWLANE (row-lane
- * kernels: short rows over a packed R) or RP_PIPE_LONGROW (long-row wave kernels: long rows over a
- * packed R with p <= 2048, one wave per tile), *staged = 1 if the R descriptors
+ * full workspace: *pipeline = RP_PIPE_TILE (one-launch tile SpGEMM with look-back) or
+ * RP_PIPE_ROWLANE (row-lane kernel: short rows over a packed R), *staged = 1 if the R descriptors
  * are fetched by the staged gather, 0 if gathered directly, 2 if the device decides per call (auto
  * mode, rp_project_choice), *bucket_shift the staged bucket width (log2 features). Any out
  * pointer may be NULL. For logging and benchmarks; results are identical on every pipeline. */
-typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1, RP_PIPE_LONGROW = 2 } rp_pipeline;
+typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1 } rp_pipeline;
 int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t* pipeline, int32_t* staged,
                     int32_t* bucket_shift);
 

@@ -1211,372 +1211,6 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
 }
 
 // ------------------------------------------------------------------------------------------
-// Long-row wave pipeline (lrw_*): packed R with p <= kLrwPMax and long rows
-// (configs[3]: 100 entries, ~32 products per row). Every wave is its own tile of `rpt` consecutive
-// rows, taken in dispatch order from the tile counter, and runs scipy's csr_matmat on each row with
-// no block barrier:
-//   * the tile's entries as ONE flat stream in rounds of 64 lanes (A and W loads of 8 rounds in
-//     flight together), products in (row, jj, kk) order into a wave buffer; a row-start bitmap gives
-//     each row's first product; sequence number q = position within the row;
-//   * first touch per column by ONE LDS atomicMax per product on a direct-mapped table of p words
-//     (key = row tag << 16 | 0xffff - q: among the current row's keys the largest is the smallest
-//     q; older rows' keys are smaller, so nothing is cleared between rows): a product leads iff the
-//     table holds its own key once its round's atomics are done (later rounds only add larger q);
-//   * a leader's sum starts at +0 + its product; the (rare) later products of its column are added
-//     in sequence order by one lane; kept = sum != 0 (NaN kept, +-0 dropped); scipy's order =
-//     descending leader q (reverse first touch), or ascending column (a p-bit map, popcounts);
-//   * the kept entries are compacted to the front of the product buffer (a row's outputs never pass
-//     its own first product), then placed with the wave-level decoupled look-back,
-//     or parked in the deferred pool exactly as the tile pipeline does (defer_copy_kernel).
-// A tile past the wave's caps (more than 64 x kLrwERounds entries or kLrwTCap products, a row of more
-// than kLrwPCap products) or finding the pool full is flagged and done by lrw_heavy_kernel (the exact
-// dense accumulator, tiles in order) before defer_copy_kernel; no wave ever waits unboundedly.
-constexpr int kLrwPCap = 256;     // products of one row on the fast path
-constexpr int kLrwTCap = 512;     // products of one wave tile (LDS buffer; the tile's output is compacted into it)
-constexpr int kLrwChunk = 8;      // entry rounds (x 64) whose loads are in flight together
-constexpr int kLrwERounds = 16;   // entries of one wave tile on the fast path: 16 x 64
-constexpr int kLrwPMax = 2048;    // columns of R (first-touch table 4 B per column, bitmap p bits)
-constexpr int kLrwRowsMax = 64;   // rows per wave tile
-
-struct LrwLayout {
-    size_t tab, bm, rs, ps, pc, pv, total;
-    __host__ __device__ LrwLayout(int p, size_t vs) {
-        auto al = [](size_t v) { return (v + 15) & ~size_t(15); };
-        tab = 0;
-        bm = al(4 * (size_t)p);
-        rs = bm + al(4 * (size_t)((p + 31) / 32));
-        ps = rs + al(8 * (size_t)kLrwERounds);
-        pc = ps + al(2 * (size_t)(kLrwRowsMax + 1));
-        pv = pc + al(2 * (size_t)kLrwTCap);
-        total = pv + al(vs * (size_t)kLrwTCap);
-    }
-};
-
-template <typename T>
-__device__ __forceinline__ T lane_value(T v, int l) {
-    return __shfl(v, l, 64);
-}
-
-template <typename T, typename IP, typename OP, typename OI>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
-lrw_main_kernel(PackedR R, T mag, int p, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
-                const T* __restrict__ Ax, OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
-                unsigned long long capacity, int rpt, int order, Workspace* ws, unsigned n_tiles,
-                uint8_t* __restrict__ tflag, DeferSpace dfr, int defer_polls, int defer_ticks) {
-    extern __shared__ __align__(16) unsigned char lds[];
-    const LrwLayout L(p, sizeof(T));
-    uint32_t* tab = reinterpret_cast<uint32_t*>(lds + L.tab);
-    uint32_t* bm = reinterpret_cast<uint32_t*>(lds + L.bm);
-    uint64_t* rsb = reinterpret_cast<uint64_t*>(lds + L.rs);   // row-start bitmap over the tile's entries
-    uint16_t* ps = reinterpret_cast<uint16_t*>(lds + L.ps);    // row -> first product; ps[nrows] = total
-    uint16_t* pcol = reinterpret_cast<uint16_t*>(lds + L.pc);
-    T* pval = reinterpret_cast<T*>(lds + L.pv);
-    unsigned long long* states = reinterpret_cast<unsigned long long*>(ws + 1);
-    const int lane = threadIdx.x;
-    const int nbw = (p + 31) >> 5;
-    for (int c = lane; c < p; c += 64) tab[c] = 0u;  // tag 0 is never a live row's tag
-    for (int c = lane; c < nbw; c += 64) bm[c] = 0u;
-    uint32_t tag = 0;
-    while (true) {
-        unsigned tile = 0;
-        if (lane == 0) tile = atomicAdd(&ws->tile_counter, 1u);
-        tile = (unsigned)__builtin_amdgcn_readfirstlane(__shfl((int)tile, 0, 64));
-        if (tile >= n_tiles) break;  // uniform
-        const int64_t row0 = (int64_t)tile * rpt;
-        const int nrows = (int)std::min<int64_t>(rpt, n_rows - row0);
-        // ---- the tile's entries [A0, A1) as one flat stream; row starts into a bitmap
-        const int64_t A0 = (int64_t)Ap[row0], A1 = (int64_t)Ap[row0 + nrows];
-        const int64_t ne = A1 - A0;
-        bool heavy = ne > 64 * kLrwERounds;
-        if (!heavy) {
-            for (int k = lane; k < kLrwERounds; k += 64) rsb[k] = 0ull;
-            __builtin_amdgcn_wave_barrier();
-            bool rnz = false;  // this lane's row (lane < nrows) has entries
-            if (lane < nrows) {
-                const int64_t s = (int64_t)Ap[row0 + lane] - A0;
-                const int64_t e = (int64_t)Ap[row0 + lane + 1] - A0;
-                rnz = e > s;
-                if (rnz) atomicOr(reinterpret_cast<unsigned long long*>(&rsb[s >> 6]), 1ull << (s & 63));
-            }
-            __builtin_amdgcn_wave_barrier();
-            // ---- products of every entry in (row, jj, kk) order = flat entry order; the
-            // product offset of each row's first entry goes to ps[row]
-            const int nr = (int)((ne + 63) >> 6);
-            uint32_t P = 0, rows_seen = 0;
-            const T* __restrict__ Axt = Ax + A0;
-            const int32_t* __restrict__ Ajt = Aj + A0;
-            for (int c0 = 0; c0 < nr && !heavy; c0 += kLrwChunk) {
-                int32_t jr[kLrwChunk];
-                T xr[kLrwChunk];
-                uint64_t wr[kLrwChunk];
-#pragma unroll
-                for (int u = 0; u < kLrwChunk; ++u) {
-                    if (c0 + u < nr) {
-                        const int64_t e = std::min<int64_t>(64 * (c0 + u) + lane, ne - 1);
-                        jr[u] = Ajt[e];
-                        xr[u] = Axt[e];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kLrwChunk; ++u)
-                    if (c0 + u < nr) wr[u] = R.W[jr[u]];
-#pragma unroll
-                for (int u = 0; u < kLrwChunk; ++u) {
-                    if (c0 + u >= nr) break;
-                    const int k = c0 + u;
-                    const bool ve = 64 * k + lane < ne;
-                    const uint32_t n = (uint32_t)(wr[u] >> 61);
-                    uint64_t d = wr[u];
-                    uint32_t cnt = n;
-                    if (n == 7) {  // more than 4 entries: the record in O (rare)
-                        const uint64_t rec = wr[u] & kLow61;
-                        cnt = R.O[rec];
-                        d = kOvf | (rec + 1);
-                    }
-                    cnt = ve ? cnt : 0u;
-                    const uint32_t inc = wave_scan_dpp(cnt);
-                    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
-                    if (P + tot > (uint32_t)kLrwTCap) {  // uniform
-                        heavy = true;
-                        break;
-                    }
-                    const uint32_t q0 = P + inc - cnt;
-                    const uint64_t fw = rsb[k];
-                    if (ve && ((fw >> lane) & 1ull)) {  // a row's first entry: its row index, its start
-                        const uint32_t rr = rows_seen + (uint32_t)__popcll(fw & ((1ull << lane) - 1ull));
-                        ps[rr] = (uint16_t)q0;
-                    }
-                    rows_seen += (uint32_t)__popcll(fw);
-                    for (uint32_t t = 0; t < cnt; ++t) {
-                        uint32_t col;
-                        T v;
-                        r_product<T>(R, mag, d, t, xr[u], col, v);
-                        pcol[q0 + t] = (uint16_t)col;
-                        pval[q0 + t] = v;
-                    }
-                    P += tot;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            // ps[k] holds the start of the k-th NONEMPTY row: spread the starts over all rows, an
-            // empty row starting where the next nonempty row starts (or at P)
-            if (!heavy) {
-                const uint64_t nz = __ballot(rnz);
-                uint32_t mine = P;
-                if (rnz) mine = ps[(uint32_t)__popcll(nz & ((1ull << lane) - 1ull))];
-                __builtin_amdgcn_wave_barrier();
-                const uint64_t after = nz & ~((2ull << lane) - 1ull);
-                const int nx = after ? __builtin_ctzll(after) : 64;
-                const uint32_t nxt = (uint32_t)__shfl((int)mine, nx & 63, 64);
-                const uint32_t start = rnz ? mine : (nx < 64 ? nxt : P);
-                if (lane <= nrows) ps[lane] = (uint16_t)(lane < nrows ? start : P);
-                __builtin_amdgcn_wave_barrier();
-            }
-            // ---- per row: first touch, leaders' sums in sequence order, kept entries compacted
-            // to the front of the product buffer in the row's output order
-            uint32_t obase = 0;
-            for (int i = 0; i < nrows && !heavy; ++i) {
-                if (++tag == 0x10000u) {  // tag space used up: clear the table (every ~65K rows of a wave)
-                    __builtin_amdgcn_wave_barrier();
-                    for (int c = lane; c < p; c += 64) tab[c] = 0u;
-                    tag = 1;
-                    __builtin_amdgcn_wave_barrier();
-                }
-                const uint32_t r0 = ps[i], r1 = ps[i + 1];
-                const uint32_t Pr = r1 - r0;
-                if (Pr > (uint32_t)kLrwPCap) {  // uniform
-                    heavy = true;
-                    break;
-                }
-                const int np = (int)((Pr + 63) >> 6);
-                uint64_t lead[kLrwPCap / 64];
-                uint32_t cq[kLrwPCap / 64];
-#pragma unroll
-                for (int v = 0; v < kLrwPCap / 64; ++v) {
-                    lead[v] = 0;
-                    cq[v] = 0;
-                    if (v >= np) continue;
-                    const uint32_t q = 64u * v + lane;
-                    const bool vq = q < Pr;
-                    const uint32_t c = vq ? pcol[r0 + q] : 0u;
-                    const T val = vq ? pval[r0 + q] : T(0);
-                    cq[v] = c;
-                    const uint32_t key = (tag << 16) | (0xffffu - q);
-                    if (vq) atomicMax(&tab[c], key);
-                    __builtin_amdgcn_wave_barrier();
-                    const uint32_t first = vq ? tab[c] : 0u;
-                    const bool isl = vq && first == key;
-                    lead[v] = __ballot(isl);
-                    if (isl) pval[r0 + q] = tadd<T>(T(0), val);
-                    const uint32_t lq = 0xffffu - (first & 0xffffu);  // the leader of this product's column
-                    uint64_t nl = __ballot(vq && !isl);
-                    __builtin_amdgcn_wave_barrier();
-                    while (nl) {  // rare: products of an already-touched column, in sequence order
-                        const int l = __builtin_ctzll(nl);
-                        nl &= nl - 1;
-                        const uint32_t Lq = (uint32_t)__builtin_amdgcn_readlane((int)lq, l);
-                        const T lv = lane_value<T>(val, l);
-                        if (lane == 0) pval[r0 + Lq] = tadd<T>(pval[r0 + Lq], lv);
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                }
-                uint64_t keep[kLrwPCap / 64];
-                T kv[kLrwPCap / 64];
-                uint32_t K = 0;
-#pragma unroll
-                for (int v = 0; v < kLrwPCap / 64; ++v) {
-                    keep[v] = 0;
-                    kv[v] = T(0);
-                    if (v >= np) continue;
-                    const bool isl = (lead[v] >> lane) & 1ull;
-                    kv[v] = isl ? pval[r0 + 64u * v + lane] : T(0);
-                    keep[v] = __ballot(isl && kv[v] != T(0));
-                    K += (uint32_t)__popcll(keep[v]);
-                }
-                __builtin_amdgcn_wave_barrier();  // every read of the row's slots is done: compact
-                if (order == RP_ORDER_SORTED) {
-#pragma unroll
-                    for (int v = 0; v < kLrwPCap / 64; ++v)
-                        if (v < np && ((keep[v] >> lane) & 1ull)) atomicOr(&bm[cq[v] >> 5], 1u << (cq[v] & 31));
-                    __builtin_amdgcn_wave_barrier();
-                    const uint32_t wbits = lane < nbw ? bm[lane] : 0u;
-                    const uint32_t wc = (uint32_t)__popc(wbits);
-                    const uint32_t wpre = wave_scan_dpp(wc) - wc;
-#pragma unroll
-                    for (int v = 0; v < kLrwPCap / 64; ++v) {
-                        if (v >= np) continue;
-                        const bool kq = (keep[v] >> lane) & 1ull;
-                        const uint32_t c = cq[v];
-                        const uint32_t pw = (uint32_t)__shfl((int)wpre, (int)(c >> 5), 64);
-                        const uint32_t word = (uint32_t)__shfl((int)wbits, (int)(c >> 5), 64);
-                        if (kq) {
-                            const uint32_t pos = pw + (uint32_t)__popc(word & ((1u << (c & 31)) - 1u));
-                            pcol[obase + pos] = (uint16_t)c;
-                            pval[obase + pos] = kv[v];
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    if (lane < nbw) bm[lane] = 0u;
-                } else {
-                    uint32_t after = 0;  // kept entries in later rounds
-#pragma unroll
-                    for (int v = kLrwPCap / 64 - 1; v >= 0; --v) {
-                        if (v >= np) continue;
-                        const uint64_t above = lane == 63 ? 0ull : keep[v] >> (lane + 1);
-                        if ((keep[v] >> lane) & 1ull) {
-                            const uint32_t pos = after + (uint32_t)__popcll(above);
-                            pcol[obase + pos] = (uint16_t)cq[v];
-                            pval[obase + pos] = kv[v];
-                        }
-                        after += (uint32_t)__popcll(keep[v]);
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                if (lane == 0) ps[i] = (uint16_t)obase;  // now the row's output offset in the tile
-                obase += K;
-                __builtin_amdgcn_wave_barrier();
-            }
-            if (!heavy) {
-                if (lane == 0) ps[nrows] = (uint16_t)obase;
-                __builtin_amdgcn_wave_barrier();
-                const unsigned long long g = lookback_wave(states, tile, obase, ws, defer_polls, true, defer_ticks);
-                if (g == ~0ull) {  // no prefix within the budget: park in the pool (or leave it to the heavy kernel)
-                    unsigned long long o = 0;
-                    if (lane == 0) {
-                        o = atomicAdd(&ws->pool_used, (unsigned long long)obase);
-                        if (o + obase <= dfr.pool_cap) {
-                            dfr.pofs[tile] = o;
-                            dfr.list[atomicAdd(&ws->n_deferred, 1u)] = tile;
-                        } else {
-                            o = ~0ull;
-                            tflag[tile] = 2;  // aggregate already published
-                        }
-                    }
-                    o = __shfl(o, 0, 64);
-                    if (o != ~0ull) {
-                        uint16_t* hd = dfr.hdr + (size_t)tile * (rpt + 1);
-                        for (int r = lane; r <= nrows; r += 64) hd[r] = ps[r];
-                        uint16_t* __restrict__ pc = dfr.cols + o;
-                        T* __restrict__ pv = reinterpret_cast<T*>(dfr.vals) + o;
-                        for (uint32_t q = lane; q < obase; q += 64) {
-                            pc[q] = pcol[q];
-                            pv[q] = pval[q];
-                        }
-                    }
-                } else {
-                    for (int r = lane; r < nrows; r += 64) Cp[row0 + r] = (OP)(g + ps[r]);
-                    if (g + obase <= capacity)
-                        for (uint32_t q = lane; q < obase; q += 64) {
-                            Cj[g + q] = (OI)pcol[q];
-                            Cx[g + q] = pval[q];
-                        }
-                    if (tile == n_tiles - 1 && lane == 0) {
-                        Cp[n_rows] = (OP)(g + obase);
-                        ws->total = g + obase;
-                    }
-                }
-            }
-        }
-        if (heavy && lane == 0) tflag[tile] = 1;  // lrw_heavy_kernel does this tile (nothing published here)
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// Tiles the wave kernel flagged: the exact dense accumulator (heavy_tile) counts, looks back
-// (blocking: every predecessor has published at least its aggregate, flagged ones in this kernel
-// before it — tiles are taken in order, 256 consecutive tiles per workgroup step) and writes.
-template <typename T, typename IP, typename OP, typename OI>
-__global__ void __launch_bounds__(kBlock)
-lrw_heavy_kernel(PackedR R, T mag, int p, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
-                 const T* __restrict__ Ax, OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
-                 unsigned long long capacity, int rpt, int order, Workspace* ws, unsigned n_tiles,
-                 const uint8_t* __restrict__ tflag) {
-    extern __shared__ __align__(16) unsigned char lds[];
-    __shared__ uint32_t s_wsum[kBlock / 64];
-    __shared__ unsigned long long s_off;
-    __shared__ uint64_t s_mask[kBlock / 64];
-    unsigned long long* states = reinterpret_cast<unsigned long long*>(ws + 1);
-    const int tid = threadIdx.x;
-    uint32_t* s_rowc = reinterpret_cast<uint32_t*>(lds + heavy_lds_bytes(p, sizeof(T)) - 4 * kBlock);
-    for (unsigned base = blockIdx.x * kBlock; base < n_tiles; base += gridDim.x * kBlock) {
-        const unsigned t = base + tid;
-        const uint8_t f = t < n_tiles ? tflag[t] : 0;
-        const uint64_t m = __ballot(f != 0);
-        if ((tid & 63) == 0) s_mask[tid >> 6] = m;
-        __syncthreads();
-        for (int wv = 0; wv < kBlock / 64; ++wv) {
-            uint64_t mm = s_mask[wv];
-            while (mm) {  // flagged tiles of this step, in order
-                const int b = __builtin_ctzll(mm);
-                mm &= mm - 1;
-                const unsigned tile = base + 64u * wv + b;
-                const bool publish = tflag[tile] == 1;
-                const int64_t row0 = (int64_t)tile * rpt;
-                const int nrows = (int)std::min<int64_t>(rpt, n_rows - row0);
-                heavy_tile<T, IP, OP, OI, PackedR>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 0, 0,
-                                                   Cp, Cj, Cx, false, order);
-                uint32_t tile_c;
-                (void)block_excl_scan(tid < nrows ? s_rowc[tid] : 0u, s_wsum, &tile_c);
-                if (tid < 64) {
-                    const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, publish);
-                    if (tid == 0) s_off = g;
-                }
-                __syncthreads();
-                const unsigned long long G = s_off;
-                heavy_tile<T, IP, OP, OI, PackedR>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 1, G,
-                                                   Cp, Cj, Cx, G + tile_c <= capacity, order);
-                if (tile == n_tiles - 1 && tid == 0) {
-                    Cp[n_rows] = (OP)(G + tile_c);
-                    ws->total = G + tile_c;
-                }
-                __syncthreads();
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// ------------------------------------------------------------------------------------------
 // Row-lane pipeline (packed R, short rows — KDD2012: 11 entries, 6 products/row).
 // No look-back and no waiting: every wave's output goes to a fixed slot, then one scan and one copy.
 //   lpr_main_kernel   one workgroup per tile of 256 rows, one wave per 64 rows. The tile's R
@@ -2850,7 +2484,7 @@ struct rp_projector {
     int stage_mode = -1; // -1 auto, 0 off, 1 on (rp_projector_set_staging)
     int stage_sb = 0;    // bucket = 2^sb features; 0 = auto
     // rp_projector_set_option (tuning and tests; the library reads no environment variables)
-    int opt_pipeline = 0;       // 0 auto, 1 tile, 2 row-lane, 3 long-row wave (where it can run)
+    int opt_pipeline = 0;       // 0 auto, 1 tile, 2 row-lane where it can run
     int opt_defer_polls = -2;   // -2 default (time budget), -1 never defer, n >= 0 polls
     int opt_defer_ticks = -1;   // -1 default
     int64_t opt_chunk_rows = 0; // 0 default
@@ -2910,9 +2544,6 @@ struct Plan {
            d = 0, sx = 0;
     unsigned long long pool_cap = 0;
     size_t total = 0;
-    // long-row wave pipeline (lrw_*): wave tiles of caps.rpt rows, tile flags for the heavy kernel
-    bool lrw = false;
-    size_t tflag = 0;
     // row-lane pipeline (lpr_*): tiles of kLprRows rows, every tile's output in a fixed slot
     bool lpr = false;
     uint32_t lpr_slot = 0;
@@ -2962,49 +2593,11 @@ bool lpr_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
     return kLprAuto && fits;
 }
 
-// Long-row wave pipeline choice: packed R with p <= kLrwPMax, rows of at least kLrwMinRow entries
-// on average (configs[3]: 100), a product count per row the wave buffer holds with room to spare.
-constexpr double kLrwMinRow = 24.0;
-bool lrw_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
-    if (h->layout != RP_LAYOUT_PACKED || h->p > kLrwPMax || n_rows <= 0 || nnz_a < 0) return false;
-    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
-    const double avg = (double)nnz_a / (double)n_rows;
-    const bool fits = avg <= 640.0 && avg * ppe <= kLrwPCap / 2.0;
-    if (h->opt_pipeline == 1 || h->opt_pipeline == 2) return false;  // tile / row-lane forced
-    if (h->opt_pipeline == 3) return fits;                             // long-row wave forced
-    return fits && avg >= kLrwMinRow;
-}
-
 Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_stage = true,
                int vs = 8, bool allow_defer = true) {
     Plan pl;
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
     auto al = [](size_t v) { return (v + 255) & ~size_t(255); };
-    if (!lpr_wanted(h, n_rows, nnz_a) && lrw_wanted(h, n_rows, nnz_a) && allow_defer) {
-        // one wave per tile of rpt rows: <= 256 expected products (the buffer holds kLrwTCap = 512)
-        // and <= 640 expected entries (kLrwERounds x 64 = 1024 on the fast path)
-        pl.lrw = true;
-        const double arow = std::max(1.0, (double)nnz_a / (double)n_rows);
-        const double prow = std::max(1.0, arow * ppe);
-        pl.caps.rpt = (int)std::max(1.0, std::min({(double)kLrwRowsMax, std::floor(256.0 / prow),
-                                                   std::floor(640.0 / arow)}));
-        pl.caps.cap_a = 0;
-        pl.caps.cap_p = 0;
-        pl.n_tiles = (n_rows + pl.caps.rpt - 1) / pl.caps.rpt;
-        pl.head = al(sizeof(Workspace) + 8u * (size_t)pl.n_tiles);  // header + look-back states
-        pl.tflag = pl.head;
-        pl.zero = pl.tflag + al((size_t)pl.n_tiles);                 // ... + tile flags, zeroed per call
-        pl.total = pl.zero;
-        pl.defer = true;
-        pl.pool_cap = (unsigned long long)(1.02 * ppe * (double)nnz_a) + 65536ull;
-        pl.dlist = pl.total;
-        pl.pofs = pl.dlist + al(4 * (size_t)pl.n_tiles);
-        pl.dhdr = pl.pofs + al(8 * (size_t)pl.n_tiles);
-        pl.pcols = pl.dhdr + al(2 * (size_t)(pl.caps.rpt + 1) * (size_t)pl.n_tiles);
-        pl.pvals = pl.pcols + al(2 * (size_t)pl.pool_cap);
-        pl.total = pl.pvals + al((size_t)vs * (size_t)pl.pool_cap);
-        return pl;
-    }
     if (lpr_wanted(h, n_rows, nnz_a) && allow_defer) {
         // one lane per row: 256-row tiles, entries capped for LDS (6 sigma), the output slot for the
         // expected products + 7.5 sigma (a tile beyond either takes the exact heavy path)
@@ -3287,57 +2880,12 @@ int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, con
     return RP_OK;
 }
 
-// the long-row wave pipeline: wave kernel (persistent: as many one-wave workgroups as fit), the
-// heavy kernel for flagged tiles, then the deferred-tile copy
-template <typename T, typename IP, typename OP, typename OI>
-int launch_lrw(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
-               Workspace* ws, const Plan& pl, hipStream_t st) {
-    char* base = reinterpret_cast<char*>(ws);
-    DeferSpace dfr{reinterpret_cast<unsigned int*>(base + pl.dlist),
-                   reinterpret_cast<unsigned long long*>(base + pl.pofs),
-                   reinterpret_cast<uint16_t*>(base + pl.dhdr), reinterpret_cast<uint16_t*>(base + pl.pcols),
-                   reinterpret_cast<unsigned char*>(base + pl.pvals), pl.pool_cap};
-    uint8_t* tflag = reinterpret_cast<uint8_t*>(base + pl.tflag);
-    const unsigned n_tiles = (unsigned)pl.n_tiles;
-    const int p = (int)h->p;
-    const size_t lds = LrwLayout(p, sizeof(T)).total;
-    const void* fn = (const void*)lrw_main_kernel<T, IP, OP, OI>;
-    HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    // persistent waves: as many as a CU can hold (32 waves; a wave that finds no tile exits at once)
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 1) cus = 256;
-    const unsigned grid = (unsigned)std::min<int64_t>((int64_t)32 * cus, (int64_t)n_tiles);
-    hipLaunchKernelGGL((lrw_main_kernel<T, IP, OP, OI>), dim3(grid), dim3(64), lds, st, R, mag, p, a->n_rows,
-                       (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr, (OI*)c->indices,
-                       (T*)c->data, (unsigned long long)c->capacity, pl.caps.rpt, order, ws, n_tiles, tflag, dfr,
-                       // a wave never waits without bound (a flagged predecessor publishes only in the
-                       // heavy kernel): "never defer" (-1) becomes a long finite poll budget here
-                       std::max(defer_polls_setting(h, pl.caps), -1) < 0 ? 4096 : defer_polls_setting(h, pl.caps),
-                       defer_ticks_setting(h, pl.caps));
-    HIP_TRY(hipGetLastError());
-    const size_t hl = heavy_lds_bytes(p, sizeof(T));
-    HIP_TRY(hipFuncSetAttribute((const void*)lrw_heavy_kernel<T, IP, OP, OI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)hl));
-    const unsigned hgrid = (unsigned)std::min<int64_t>(((int64_t)n_tiles + kBlock - 1) / kBlock, 1024);
-    hipLaunchKernelGGL((lrw_heavy_kernel<T, IP, OP, OI>), dim3(hgrid), dim3(kBlock), hl, st, R, mag, p, a->n_rows,
-                       (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr, (OI*)c->indices,
-                       (T*)c->data, (unsigned long long)c->capacity, pl.caps.rpt, order, ws, n_tiles,
-                       (const uint8_t*)tflag);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, kDeferCopyGrid)), dim3(kBlock), 0, st, dfr,
-                       ws, pl.caps, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices, (T*)c->data,
-                       (unsigned long long)c->capacity);
-    HIP_TRY(hipGetLastError());
-    return RP_OK;
-}
-
 template <typename T, typename IP, typename OP, typename OI, typename RL>
 int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
                  int order, Workspace* ws, unsigned n_tiles, const Plan& pl, size_t lds,
                  hipStream_t st) {
     if constexpr (std::is_same<RL, PackedR>::value) {
         if (pl.lpr) return launch_lpr<T, IP, OP, OI>(R, mag, h, a, c, order, ws, pl, st);
-        if (pl.lrw) return launch_lrw<T, IP, OP, OI>(R, mag, h, a, c, order, ws, pl, st);
         if (pl.staged) {
             char* base = reinterpret_cast<char*>(ws);
             int64_t* TE = reinterpret_cast<int64_t*>(base + pl.te);
@@ -3432,9 +2980,8 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
             plan = make_plan(h, a->n_rows, nnz_a_hint, false, vs, false);
     }
     const Caps& caps = plan.caps;
-    const size_t lds = plan.lpr   ? std::max(lpr_lds_bytes(caps.cap_a, (size_t)vs, plan.lpr_slot, plan.staged), heavy_lds_bytes(h->p, (size_t)vs))
-                       : plan.lrw ? std::max(LrwLayout((int)h->p, (size_t)vs).total, heavy_lds_bytes(h->p, (size_t)vs))
-                                  : lds_bytes_for(caps, dtype_size(a->data_type), h->p);
+    const size_t lds = plan.lpr ? std::max(lpr_lds_bytes(caps.cap_a, (size_t)vs, plan.lpr_slot, plan.staged), heavy_lds_bytes(h->p, (size_t)vs))
+                                : lds_bytes_for(caps, dtype_size(a->data_type), h->p);
     if (lds > 160 * 1024 - 4096)
         return fail(RP_ERR_UNSUPPORTED, "p=%lld too large for the LDS accumulator (%zu bytes)",
                     (long long)h->p, lds);
@@ -3836,7 +3383,7 @@ int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_
                     int32_t* bucket_shift) {
     if (!h || n_rows < 0) return fail(RP_ERR_INVALID, "NULL projector or n_rows < 0");
     const Plan pl = make_plan(h, n_rows, nnz_a);
-    if (pipeline) *pipeline = pl.lpr ? RP_PIPE_ROWLANE : pl.lrw ? RP_PIPE_LONGROW : RP_PIPE_TILE;
+    if (pipeline) *pipeline = pl.lpr ? RP_PIPE_ROWLANE : RP_PIPE_TILE;
     if (staged) *staged = pl.gated ? 2 : pl.staged ? 1 : 0;
     if (bucket_shift) *bucket_shift = pl.staged ? pl.sb : 0;
     return RP_OK;
@@ -3877,8 +3424,7 @@ int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value) {
     if (!h) return fail(RP_ERR_INVALID, "NULL projector");
     switch (option) {
         case RP_OPT_PIPELINE:
-            if (value < 0 || value > 3)
-                return fail(RP_ERR_INVALID, "pipeline must be 0 (auto), 1 (tile), 2 (row-lane) or 3 (long-row wave)");
+            if (value < 0 || value > 2) return fail(RP_ERR_INVALID, "pipeline must be 0 (auto), 1 (tile) or 2 (row-lane)");
             h->opt_pipeline = (int)value;
             return RP_OK;
         case RP_OPT_DEFER_POLLS:

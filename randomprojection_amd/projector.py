@@ -321,7 +321,7 @@ class Projector:
         pipe, st, sb = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         nat.check(self._lib.rp_project_plan(self._h, int(n_rows), int(nnz_a), ctypes.byref(pipe), ctypes.byref(st),
                                             ctypes.byref(sb)))
-        return {"pipeline": {0: "tile", 1: "rowlane", 2: "longrow"}[pipe.value],
+        return {"pipeline": "rowlane" if pipe.value == 1 else "tile",
                 "staged": "auto" if st.value == 2 else bool(st.value), "bucket_shift": int(sb.value)}
 
     def choice(self, n_rows: int, nnz_a: int, workspace) -> bool:
@@ -341,11 +341,11 @@ class Projector:
                 "defer_ticks": nat.RP_OPT_DEFER_TICKS, "chunk_rows": nat.RP_OPT_CHUNK_ROWS,
                 "host_threads": nat.RP_OPT_HOST_THREADS}
     _OPTION_DEFAULTS = {"pipeline": 0, "defer_polls": -2, "defer_ticks": -1, "chunk_rows": 0, "host_threads": -1}
-    _PIPELINES = {"auto": 0, "tile": 1, "rowlane": 2, "longrow": 3}
+    _PIPELINES = {"auto": 0, "tile": 1, "rowlane": 2}
 
     def set_option(self, name: str, value):
         """Tuning / test option of this projector (rp_projector_set_option; results are identical
-        under every setting): pipeline ("auto" | "tile" | "rowlane" | "longrow"), defer_polls, defer_ticks,
+        under every setting): pipeline ("auto" | "tile" | "rowlane"), defer_polls, defer_ticks,
         chunk_rows, host_threads; ``None`` restores the default."""
         if name not in self._OPTIONS:
             raise ValueError(f"unknown option {name!r}; one of {sorted(self._OPTIONS)}")

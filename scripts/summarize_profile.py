@@ -28,8 +28,8 @@ STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel", "stage_partition_
                 "lpr_count_kernel", "lpr_run_scan_kernel", "lpr_seg_scan_kernel", "lpr_partition_kernel",
                 "lpr_gather_kernel", "lpr_main_kernel", "lpr_main_flat_kernel", "lpr_choose_kernel",
                 "lpr_heavy_count_kernel", "lpr_scan_kernel",
-                "lpr_copy_kernel", "lpr_heavy_write_kernel", "lrw_main_kernel", "lrw_heavy_kernel")
-MAIN_KERNELS = ("lpr_main_kernel", "lpr_main_flat_kernel", "spgemm_lookback_kernel", "lrw_main_kernel")
+                "lpr_copy_kernel", "lpr_heavy_write_kernel")
+MAIN_KERNELS = ("lpr_main_kernel", "lpr_main_flat_kernel", "spgemm_lookback_kernel")
 
 
 def short(name):
