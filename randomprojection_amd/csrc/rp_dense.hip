@@ -9,11 +9,13 @@
 //   bf16: bf16 operands, f32 accumulate, f32 result (v_mfma_f32_16x16x32_bf16 / _32x32x16_bf16).
 //   f32:  exact f32 products (gfx950 has no xf32), f32 accumulate (v_mfma_f32_16x16x4_f32 / _32x32x2_f32).
 //
-// Two kernel families (rp_dense_set_variant picks one for measurements):
-//  * dense_glds_kernel (variant 10, the default): 256 x 256 tile, 8 waves of 128 x 64, 16 x 16
-//    MFMAs, operands staged global -> LDS by global_load_lds_dwordx4 (no VGPR round trip), XOR
-//    swizzle applied on the source address, two K-tile buffers with the next K-tile in flight during
-//    this one's MFMAs (description above the kernel);
+// Kernel families (rp_dense_set_variant picks one for measurements):
+//  * dense_ring_kernel (variant 11, the default): 256 x 256 tile, 8 waves of 128 x 64, 16 x 16
+//    MFMAs, operands staged global -> LDS by global_load_lds_dwordx4 (no VGPR round trip) into a
+//    ring of four 64-B-per-row K-tile buffers, three K-tiles in flight while one is multiplied, one
+//    barrier per K-tile (description above the kernel);
+//  * dense_glds_kernel (variant 10): the same tile and staging with two 128-B-per-row buffers, the
+//    next K-tile in flight during this one's MFMAs;
 //  * dense_nt_kernel (variants 0-9; variant 5 = 256 x 256, 8 waves, 32 x 32 MFMAs, two LDS stages, the
 //    round-2 default): the next K step loaded global -> registers during the MFMAs, then written to
 //    the other LDS buffer (one barrier per step); LDS rows of 128 B XOR-swizzled (chunk c of row r at
@@ -338,6 +340,130 @@ int launch_dense_glds(const void* X, const void* G, float* Y, int64_t n, int64_t
     return RP_OK;
 }
 
+// Four-stage ring (variant 11): the same 256 x 256 tile and 8 waves of 128 x 64 in 16 x 16 MFMAs, but
+// K-tiles of 64 B per row (32 bf16 / 16 f32) in a ring of four 32 KB LDS buffers, so three K-tiles
+// are in flight while one is multiplied (the two-buffer kernel keeps one, ~1 us ahead: less than a
+// loaded HBM round trip). Per K-tile: wait for the oldest stage (vmcnt(8) with two younger stages
+// still in flight), one barrier, issue the K-tile three ahead into the buffer everyone finished,
+// then one MFMA substep (bf16: 32 x 16x16x32; f32: 128 x 16x16x4 over the lane groups' 4 k each).
+// LDS rows of 4 chunks; chunk c of row r at c ^ F(r), F(r) = -(r >> 2) & 3, which makes each of
+// ds_read_b128's 16-lane groups hit 16 distinct 16-B bank slots (rows 16 B x 4 apart share banks
+// only across groups).
+template <bool BF16>
+__global__ void __launch_bounds__(512)
+dense_ring_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, float* __restrict__ C,
+                  int64_t M, int N, int K, int64_t ldc, unsigned m_tiles, unsigned n_tiles) {
+    constexpr int BM = 256, BN = 256, KC = 4, NS = 4;  // KC: 16-B chunks per 64-B row slice
+    constexpr int ES = BF16 ? 2 : 4, KT = 64 / ES;     // element size, elements per K-tile
+    constexpr int SZ = (BM + BN) * KC;                  // chunks per stage
+    __shared__ uint4 lds[NS * SZ];                      // 4 x 32 KB
+    const unsigned bi = blockIdx.x, xcd = bi & 7u, j = bi >> 3;
+    const unsigned mt = (j / n_tiles) * 8u + xcd, nt = j % n_tiles;
+    if (mt >= m_tiles) return;  // uniform
+    const int64_t m0 = (int64_t)mt * BM;
+    const int n0 = (int)nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 2, wn = w & 3;
+    const int steps = K / KT;
+    auto F = [](int r) { return (4 - ((r >> 2) & 3)) & 3; };
+    // staging: instruction i moves LDS chunks [i * 512 + 64 w, + 64) = rows i * 128 + tid / 4
+    const int srow = tid >> 2, sxc = (tid & 3) ^ F(srow);
+    const char* ga[2];
+    const char* gb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int64_t ra = std::min<int64_t>(m0 + i * 128 + srow, M - 1);
+        const int rb = std::min(n0 + i * 128 + srow, N - 1);
+        ga[i] = reinterpret_cast<const char*>(Av) + (ra * (int64_t)K + sxc * (16 / ES)) * ES;
+        gb[i] = reinterpret_cast<const char*>(Bv) + ((int64_t)rb * K + sxc * (16 / ES)) * ES;
+    }
+    // global_load_lds_dwordx4 issued as inline asm: the compiler does not see these LDS writes, so
+    // it inserts no vmcnt(0) before this wave's ds_reads or the barrier (it would wait for all
+    // three stages in flight); the vmcnt waits below are explicit. M0 = the wave's LDS destination.
+    const uint32_t lds0 = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)reinterpret_cast<uintptr_t>(lds + 64 * w));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: the clobber keeps the compiler's own uses safe
+    auto dma = [&](const char* g, uint32_t l) {
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+    };
+#pragma clang diagnostic pop
+    auto stage = [&](int kt) {
+        const uint32_t base = lds0 + (uint32_t)((kt & (NS - 1)) * SZ) * 16u;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dma(ga[i] + (int64_t)kt * 64, base + i * 512 * 16);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dma(gb[i] + (int64_t)kt * 64, base + (BM * KC + i * 512) * 16);
+    };
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int kt = 0; kt < NS - 1 && kt < steps; ++kt) stage(kt);
+    for (int kt = 0; kt < steps; ++kt) {
+        // K-tile kt landed (this wave's loads; the barrier: everyone's); younger stages stay in flight
+        if (kt + 2 < steps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (kt + 1 < steps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + NS - 1 < steps) stage(kt + NS - 1);  // into the buffer of K-tile kt - 1: all done with it
+        const uint4* sa = lds + (kt & (NS - 1)) * SZ;
+        const uint4* sb = sa + BM * KC;
+        uint4 bfr[4];
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int r = wn * 64 + ni * 16 + fr;
+            bfr[ni] = sb[r * KC + (fq ^ F(r))];
+        }
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+            const int r = wm * 128 + mi * 16 + fr;
+            const uint4 afr = sa[r * KC + (fq ^ F(r))];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                if constexpr (BF16) {
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        __builtin_bit_cast(bf16x8s, afr), __builtin_bit_cast(bf16x8s, bfr[ni]), acc[mi][ni], 0, 0, 0);
+                } else {
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(afr.x), __uint_as_float(bfr[ni].x),
+                                                                      acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(afr.y), __uint_as_float(bfr[ni].y),
+                                                                      acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(afr.z), __uint_as_float(bfr[ni].z),
+                                                                      acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(afr.w), __uint_as_float(bfr[ni].w),
+                                                                      acc[mi][ni], 0, 0, 0);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int c = n0 + wn * 64 + ni * 16 + fr;
+            if (c >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + wm * 128 + mi * 16 + 4 * fq + r;
+                if (row < M) C[row * ldc + c] = acc[mi][ni][r];
+            }
+        }
+}
+
+template <bool BF16>
+int launch_dense_ring(const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
+                      hipStream_t st) {
+    const unsigned m_tiles = (unsigned)((n + 255) / 256), n_tiles = (unsigned)((p + 255) / 256);
+    const uint64_t blocks = (uint64_t)((m_tiles + 7) / 8) * 8ull * n_tiles;
+    if (blocks >= (1ull << 31)) return fail(RP_ERR_UNSUPPORTED, "too many rows for one launch");
+    hipLaunchKernelGGL((dense_ring_kernel<BF16>), dim3((unsigned)blocks), dim3(512), 0, st, X, G, Y, n, (int)p, (int)m,
+                       ldy, m_tiles, n_tiles);
+    HIP_TRY(hipGetLastError());
+    return RP_OK;
+}
+
 // f64 (sklearn computes in X's dtype): v_mfma_f64_16x16x4_f64 — lane l supplies A[row l & 15][k = l >> 4]
 // (one double), C/D: col l & 15, row (l >> 4) + 4 r (NOT the f32 map). Tile 256 x 128, 8 waves (4 M x
 // 2 N) of 64 x 64 = 4 x 4 MFMA tiles (128 accumulator VGPRs); K-tile = 128 B of a row = 16 doubles; a
@@ -455,13 +581,15 @@ int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, i
 // tile variants (RP_DENSE_VARIANT, measurements): 0 = 128x128 2 stages, 1 = 128x128 1 stage,
 // 2 = 256x128 1 stage, 3 = 128x256 2 stages (8 waves), 4 = 256x256 1 stage (8 waves), 5 = 256x256
 // 2 stages (128 KB LDS, 8 waves)
-// defaults: the LDS-direct 256 x 256 kernel for both (measured, profiles/r03_dense_*: bf16 975-1221 TF
-// vs 353 for variant 5; f32 133 TF vs 97)
-constexpr int kDenseVariantBf16 = 10, kDenseVariantF32 = 10;
+// defaults: the four-stage LDS-direct ring for both (measured, profiles/r03_dense_*: bf16 1114 TF vs
+// 980 for the two-buffer kernel (variant 10) and 353 for variant 5; f32 145 TF vs 133 and 97;
+// hipBLASLt on the same shapes 1302 / 154 TF)
+constexpr int kDenseVariantBf16 = 11, kDenseVariantF32 = 11;
 template <typename T>
 int dispatch_dense(int v, const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
                    hipStream_t st) {
     if (v == 10) return launch_dense_glds<std::is_same<T, uint16_t>::value>(X, G, Y, n, m, p, ldy, st);
+    if (v == 11) return launch_dense_ring<std::is_same<T, uint16_t>::value>(X, G, Y, n, m, p, ldy, st);
     switch (v) {
         case 1: return launch_dense<T, 2, 2, 2, 2, 1>(X, G, Y, n, m, p, ldy, st);
         case 2: return launch_dense<T, 2, 2, 4, 2, 1>(X, G, Y, n, m, p, ldy, st);
@@ -481,7 +609,7 @@ std::atomic<int> g_dense_variant{-1};  // rp_dense_set_variant (measurements); -
 }  // namespace
 
 extern "C" int rp_dense_set_variant(int32_t variant) {
-    if (variant < -1 || variant > 10) return fail(RP_ERR_INVALID, "variant must be -1 (default) or 0..10");
+    if (variant < -1 || variant > 11) return fail(RP_ERR_INVALID, "variant must be -1 (default) or 0..11");
     g_dense_variant.store(variant, std::memory_order_relaxed);
     return RP_OK;
 }

@@ -1603,6 +1603,7 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
                 if (j + kXP + u < nsteps) step(j + kXP + u, xw[u]);
         }
         bool overflow = carry_k > sp.slot;
+        STAMP(3);
         __syncthreads();
         // side fill: every side entry's products into its gap, in R's storage order
         if ((uint32_t)tid < nside) {
@@ -1628,16 +1629,18 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
                 }
             }
         }
-        // ---- the next tile's round 2, in flight during this tile's row phase
-        const uint32_t npre = nxt.tile < n_tiles ? stage_runs(nxt) : 0u;  // two barriers (staged)
-        __syncthreads();
+        // ---- the next tile's round 2, in flight during this tile's row phase. The run table's two
+        // barriers also publish the side fill (and s_bad) to the row phase
+        uint32_t npre = 0;
+        if (STAGED && nxt.tile < n_tiles) npre = stage_runs(nxt);
+        else __syncthreads();
         const bool bad2 = s_bad[par] != 0;  // uniform: a side entry with 15 or more products
         if (nxt.tile < n_tiles) {
             round2(nxt, 0, npre);
             first_values(nxt);
         }
         if (!skip && bad2 && tid == 0) go_heavy(tile);
-        STAMP(3);
+        STAMP(4);
         if (!skip && !bad2) {
             // ---- per row: kept count and a Bloom check of its columns (3 x 64-bit filters in
             // registers): a column whose 3 bits are all set already flags the row for the exact
@@ -1759,7 +1762,6 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
                 }
             }
         }
-        STAMP(4);
         STAMP(5);
         STAMP(6);
         if (nxt.tile >= n_tiles) break;  // uniform

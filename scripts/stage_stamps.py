@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--p", type=int, default=4096)
     ap.add_argument("--mean-extra", type=float, default=10.0)
     ap.add_argument("--rpt", type=int, default=256, help="rows per tile the launch will use")
-    ap.add_argument("--lpr", action="store_true", help="stamps of the row-lane pipeline (RP_PIPE=lpr)")
+    ap.add_argument("--lpr", action="store_true", help="stamps of the row-lane pipeline (stage names)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "stamps.json"))
     args = ap.parse_args()
 
@@ -57,7 +57,8 @@ def main():
     t0 = st[:, 0].min()
     names = ["gather-or-staged-read(1a)", "scan(1b)", "products(1c)", "accumulate(2)", "scan+lookback(3a)", "write(3b)"]
     if args.lpr:
-        names = ["descs(wait round2)", "barrier+round1-issue", "flatpass+side+next-runs", "rows+exact+slot-store", "-", "-"]
+        names = ["descs(wait round2)", "barrier+round1-issue", "flatpass", "side-fill+next-runs(3 barriers)",
+                 "rows+exact+slot-store", "-"]
     res = {"tiles": int(n_tiles), "heavy_tiles": int((st[:, 7] > 0).sum())}
     ok = st[:, 6] > 0
     for k, nm in enumerate(names):

@@ -50,7 +50,7 @@ def test_sparse_input():
     assert _rel(ours.transform(X), ref.transform(X)) < 1e-5
 
 
-@pytest.mark.parametrize("variant", [-1, 5, 10])
+@pytest.mark.parametrize("variant", [-1, 5, 10, 11])
 @pytest.mark.parametrize("compute", ["fp32", "bf16", "fp64"])
 @pytest.mark.parametrize("shape", [(1, 64, 1), (300, 4096, 200), (1000, 16384, 1024), (257, 192, 129)])
 def test_mfma_kernel_ragged_shapes(compute, shape, variant):

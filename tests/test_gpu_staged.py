@@ -254,6 +254,72 @@ def test_rowlane_staged_tile_past_one_round(R2m_p1k):
     P.close()
 
 
+def _rows(rng, k, pool, m, dtype=np.float32):
+    """CSR rows with k[i] distinct columns drawn from `pool` (ascending), normal values."""
+    k = np.asarray(k)
+    n, kmax, big = len(k), int(k.max()), np.iinfo(np.int64).max
+    valid = np.arange(kmax)[None, :] < k[:, None]
+    draw = np.full((n, kmax), big)
+    todo = np.arange(n)
+    while todo.size:  # redraw the rows that drew a column twice
+        d = np.where(valid[todo], rng.integers(0, len(pool), size=(todo.size, kmax)), big)
+        d.sort(axis=1)
+        draw[todo] = d
+        todo = todo[((np.diff(d, axis=1) == 0) & valid[todo][:, 1:]).any(axis=1)]
+    cols = np.asarray(pool, dtype=np.int64)[draw[valid]]
+    return sp.csr_matrix((rng.standard_normal(int(k.sum())).astype(dtype), cols,
+                          np.concatenate([[0], np.cumsum(k)])), shape=(n, m))
+
+
+def _check_rowlane_staged(R, A, shift):
+    want = oracle_product(A, R)
+    Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
+    P = Projector(R)
+    P.set_option("pipeline", "rowlane")
+    P.set_staging("on", shift)
+    assert P.plan(A.shape[0], A.nnz) == {"pipeline": "rowlane", "staged": True, "bucket_shift": shift}
+    assert_same_csr(P.matmul(A), *want)
+    assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
+    P.close()
+
+
+def test_rowlane_staged_tile_of_3200_live_entries(R2m_p1k):
+    """A tile of 3200 entries, all on nonempty R rows (every staged word carries products): its
+    words take two rounds of the main kernel's descriptor fetch (12 x 256 per round), the second
+    with 128 of 256 lanes in range, next to tiles of ~11 entries per row."""
+    rng = np.random.default_rng(3200)
+    R = R2m_p1k
+    m = R.shape[0]
+    live = np.flatnonzero(np.diff(R.indptr) > 0)
+    k = np.full(256, 12)
+    k[:128] = 13
+    A = sp.vstack([kdd_like(rng, 9 * 256, m, mean=11.2, values="normal"), _rows(rng, k, live, m),
+                   kdd_like(rng, 9 * 256 + 31, m, mean=11.2, values="normal")]).tocsr()
+    _check_rowlane_staged(R, A, 16)
+
+
+def test_rowlane_staged_dead_tiles_and_shared_run_starts(R2m_p1k):
+    """Tiles none of whose entries has a nonempty R row (every staged word filtered by the gather's
+    bitmap, no products), and a bucket touched only by the first and the last of ~1500 tiles: every
+    tile between has an empty run there, all with the same start in the segment. Plus empty rows."""
+    rng = np.random.default_rng(1500)
+    R = R2m_p1k
+    m = R.shape[0]
+    nzr = np.diff(R.indptr) > 0
+    shift = 13
+    b0 = np.arange(0, 1 << shift)
+    live0, dead = b0[nzr[b0]], np.flatnonzero(~nzr)
+    b1 = np.arange(1 << shift, 2 << shift)
+    live1 = b1[nzr[b1]]
+    n_tiles = 1500
+    edge = [(_rows(rng, np.full(256, 2), live0, m) + _rows(rng, np.full(256, 1), live1, m)).tocsr() for _ in range(2)]
+    A = sp.vstack([edge[0], _rows(rng, np.full(256 * 600, 3), live0, m), _rows(rng, np.full(3 * 256, 4), dead, m),
+                   sp.csr_matrix((300, m), dtype=np.float32), _rows(rng, np.full(256 * (n_tiles - 600), 3), live0, m),
+                   edge[1]]).tocsr()
+    A.sort_indices()
+    _check_rowlane_staged(R, A, shift)
+
+
 @pytest.mark.parametrize("dist", ["uniform", "powerlaw"])
 def test_auto_staging_choice_on_device(dist):
     """Auto mode on a launch large enough to stage (>= 4M entries, R's W table >= 64 MB): the device
