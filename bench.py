@@ -80,7 +80,7 @@ def step_kernels(plan, staged_run):
         ks = ["lpr_main_kernel" if staged_run else "lpr_main_flat_kernel", "lpr_heavy_count_kernel",
               "lpr_scan_kernel", "lpr_copy_kernel", "lpr_heavy_write_kernel"]
         if staged_run:
-            ks = ["lpr_count_kernel", "lpr_run_scan_kernel", "lpr_seg_scan_kernel", "lpr_partition_kernel",
+            ks = ["lpr_reserve_kernel", "lpr_partition_kernel",
                   "lpr_gather_kernel"] + ks
         if plan["staged"] == "auto":
             ks = ["lpr_choose_kernel"] + ks

@@ -926,14 +926,15 @@ stage_gather_kernel(const uint32_t* __restrict__ W32, const int64_t* __restrict_
 
 // ---- staging for the row-lane pipeline: bucket-major runs inside groups of kRunGroup tiles.
 // S holds, for tile group g and bucket b, the entries of all the group's tiles whose feature falls
-// in b as ONE contiguous segment (tile order, then rank order inside the tile); segments are laid
-// out in (g, b) order. So the gather streams whole segments (full 128-byte lines, nothing shared
-// between workgroups), and a tile's entries come back as nb runs, each adjacent to the neighbouring
-// tiles' runs of the same bucket — neighbours run on the same XCD (xcd_tile), so the lines they
-// share meet in one L2. Index arrays (workspace):
+// in b as ONE contiguous segment (one run per tile, runs in claim order, rank order inside the
+// run); segments are laid out in (g, b) order, each with a reserve sized from the group's entries
+// (lpr_reserve_kernel). So the gather streams whole segments (full 128-byte lines, nothing shared
+// between workgroups), and a tile's entries come back as nb runs. One pass over A (the partition
+// claims each run with an atomicAdd on its segment's fill); a segment past its reserve (columns far
+// from uniform) sends the call to the direct kernel. Index arrays (workspace):
 //   OFFT[b][t] (u16)  within-tile start of bucket b (bucket order), OFFT[nb][t] = the tile's entries
 //   OFF2[b][t] (u32)  start of tile t's run in segment (g, b), relative to the segment
-//   GB[g*nb + b] (i64) segment start in S (exclusive prefix; GB[groups*nb] = all staged entries)
+//   GB[g*nb + b] (i64) segment start in S (exclusive prefix of the reserves), FILL[g*nb + b] its fill
 // A tile past the entry cap stages nothing (its counts are 0): the heavy path reads A itself.
 constexpr int kRunGroup = 4096;  // tiles per group (uniform KDD2012: ~110K entries per segment)
 
@@ -974,85 +975,33 @@ lpr_choose_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int
     if (threadIdx.x == 0) *gate = S > 0 && s_new * 100u >= (uint32_t)kChooseDistinctPct * (uint32_t)S ? 1u : 0u;
 }
 
-// K1: per-tile bucket histogram -> OFFT (within-tile exclusive starts)
+// K1: segment reserves. Segment (g, b) gets room for E + 8 sqrt(E) + 256 entries, E = the group's
+// entries x bucket b's share of the features (the staged words of uniform columns are binomial
+// around E: 8 sigma); GB[s] = exclusive prefix of the reserves, FILL[s] = 0. One workgroup.
+constexpr int kResBlock = 1024;
 template <typename IP>
-__global__ void __launch_bounds__(kBlock)
-lpr_count_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, Caps caps,
-                 unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT,
-                 const uint32_t* __restrict__ gate) {
-    if (gate && *gate == 0) return;  // the device chose direct gathers for this call
-    __shared__ uint32_t s_hist[kStageMaxNB];
-    __shared__ uint32_t s_wsum[kBlock / 64];
-    const int tid = threadIdx.x;
-    const unsigned t = xcd_tile(blockIdx.x, t8);
-    if (t >= n_tiles) return;  // uniform
-    const int64_t row0 = (int64_t)t * caps.rpt;
-    const int64_t ea = (int64_t)Ap[row0];
-    const int64_t ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
-    if (ne > caps.cap_a) {
-        for (int b = tid; b <= nb; b += kBlock) OFFT[(size_t)b * ostride + t] = 0;
-        return;
-    }
-    const uint32_t n = (uint32_t)ne;
-    if (tid < nb) s_hist[tid] = 0;
-    __syncthreads();
-    const int32_t* __restrict__ Ajt = Aj + ea;
-    int32_t jj[kMaxE];
-#pragma unroll
-    for (int i = 0; i < kMaxE; ++i) {
-        const uint32_t e = tid + i * kBlock;
-        jj[i] = e < n ? Ajt[e] : -1;
-    }
-#pragma unroll
-    for (int i = 0; i < kMaxE; ++i)
-        if (jj[i] >= 0) atomicAdd(&s_hist[(uint32_t)jj[i] >> sb], 1u);
-    __syncthreads();
-    uint32_t tot;
-    const uint32_t base = block_excl_scan(tid < nb ? s_hist[tid] : 0u, s_wsum, &tot);
-    if (tid < nb) OFFT[(size_t)tid * ostride + t] = (uint16_t)base;
-    if (tid == 0) OFFT[(size_t)nb * ostride + t] = (uint16_t)n;
-}
-
-// K2: one workgroup per (group, bucket): runs of the group's tiles -> OFF2, segment size -> GB
-constexpr int kRunPer = kRunGroup / kBlock;  // tiles per thread
-__global__ void __launch_bounds__(kBlock)
-lpr_run_scan_kernel(const uint16_t* __restrict__ OFFT, uint32_t* __restrict__ OFF2, int64_t* __restrict__ GB,
-                    unsigned n_tiles, int nb, uint32_t ostride, const uint32_t* __restrict__ gate) {
-    if (gate && *gate == 0) return;
-    __shared__ uint32_t s_wsum[kBlock / 64];
-    const unsigned g = blockIdx.x / (unsigned)nb, b = blockIdx.x % (unsigned)nb;
-    const unsigned t0 = g * kRunGroup + kRunPer * threadIdx.x;
-    const uint16_t* o0 = OFFT + (size_t)b * ostride;
-    const uint16_t* o1 = o0 + ostride;
-    uint32_t c[kRunPer], sum = 0;
-#pragma unroll
-    for (int i = 0; i < kRunPer; ++i) {
-        const unsigned t = t0 + i;
-        c[i] = t < n_tiles ? (uint32_t)o1[t] - (uint32_t)o0[t] : 0u;
-        sum += c[i];
-    }
-    uint32_t tot;
-    uint32_t run = block_excl_scan(sum, s_wsum, &tot);
-#pragma unroll
-    for (int i = 0; i < kRunPer; ++i) {
-        const unsigned t = t0 + i;
-        if (t < n_tiles) OFF2[(size_t)b * ostride + t] = run;
-        run += c[i];
-    }
-    if (threadIdx.x == 0) GB[blockIdx.x] = tot;
-}
-
-// K3: segment sizes -> exclusive starts, in place (one workgroup of 1024 threads)
-__global__ void __launch_bounds__(1024) lpr_seg_scan_kernel(int64_t* __restrict__ GB, unsigned n,
-                                                            const uint32_t* __restrict__ gate) {
-    if (gate && *gate == 0) return;
-    __shared__ int64_t s[1024];
-    const unsigned per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = std::min(n, lo + per);
+__global__ void __launch_bounds__(kResBlock)
+lpr_reserve_kernel(const IP* __restrict__ Ap, int64_t n_rows, int rpt, int64_t m, unsigned groups, int sb, int nb,
+                   int64_t cap_words, int64_t* __restrict__ GB, uint32_t* __restrict__ FILL,
+                   uint32_t* __restrict__ gate) {
+    if (*gate == 0) return;  // the device chose direct gathers for this call
+    __shared__ int64_t s[kResBlock];
+    const unsigned S = groups * (unsigned)nb;
+    const unsigned per = (S + kResBlock - 1) / kResBlock, lo = threadIdx.x * per, hi = std::min(S, lo + per);
+    auto reserve = [&](unsigned sg) {
+        const unsigned g = sg / (unsigned)nb, b = sg % (unsigned)nb;
+        const int64_t r0 = std::min<int64_t>((int64_t)g * kRunGroup * rpt, n_rows);
+        const int64_t r1 = std::min<int64_t>((int64_t)(g + 1) * kRunGroup * rpt, n_rows);
+        const double ents = (double)((int64_t)Ap[r1] - (int64_t)Ap[r0]);
+        const double width = (double)std::min<int64_t>((int64_t)1 << sb, m - ((int64_t)b << sb));
+        const double e = ents * width / (double)m;
+        return (int64_t)(e + 8.0 * sqrt(e)) + 256;
+    };
     int64_t sum = 0;
-    for (unsigned i = lo; i < hi; ++i) sum += GB[i];
+    for (unsigned i = lo; i < hi; ++i) sum += reserve(i);
     s[threadIdx.x] = sum;
     __syncthreads();
-    for (unsigned o = 1; o < 1024; o <<= 1) {
+    for (unsigned o = 1; o < kResBlock; o <<= 1) {
         const int64_t v = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
         __syncthreads();
         s[threadIdx.x] += v;
@@ -1060,11 +1009,14 @@ __global__ void __launch_bounds__(1024) lpr_seg_scan_kernel(int64_t* __restrict_
     }
     int64_t run = s[threadIdx.x] - sum;
     for (unsigned i = lo; i < hi; ++i) {
-        const int64_t v = GB[i];
         GB[i] = run;
-        run += v;
+        FILL[i] = 0u;
+        run += reserve(i);
     }
-    if (threadIdx.x == 1023) GB[n] = s[1023];
+    if (threadIdx.x == kResBlock - 1) {
+        GB[S] = s[kResBlock - 1];
+        if (s[kResBlock - 1] > cap_words) *gate = 0;  // cannot happen with the planned size: direct then
+    }
 }
 
 // largest b in [0, nb] with st[b] <= q (fixed trip count: 9 probes cover nb <= 256)
@@ -1076,26 +1028,37 @@ __device__ __forceinline__ uint32_t run_of(const uint16_t* st, int nb, uint32_t 
     return lo;
 }
 
-// K4: the tile's entries ranked into bucket order in LDS, then written to their runs (consecutive
-// lanes -> consecutive S words inside a run). S word: entry index in the tile << 20 | column bits.
+// K2: partition, one workgroup per tile: the tile's entries histogrammed by bucket in LDS, the
+// within-tile bucket starts -> OFFT, each nonempty bucket's run claimed in its (group, bucket)
+// segment by one atomicAdd on FILL -> OFF2, the entries ranked into bucket order in LDS and written
+// to their runs (consecutive lanes -> consecutive S words inside a run). S word: entry index in the
+// tile << 20 | column bits. Runs land in a segment in claim order (any order: the main kernel finds
+// a tile's runs through OFF2). A run past its segment's reserve sets the gate to 0: the call's
+// remaining kernels take the direct path (lpr_main_flat_kernel). A tile past the entry cap stages
+// nothing (its counts are 0): the heavy path reads A itself.
 template <typename IP>
 __global__ void __launch_bounds__(kBlock)
 lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, Caps caps,
-                     unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride,
-                     const uint16_t* __restrict__ OFFT, const uint32_t* __restrict__ OFF2,
-                     const int64_t* __restrict__ GB, uint32_t* __restrict__ S, const uint32_t* __restrict__ gate) {
-    if (gate && *gate == 0) return;
+                     unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT,
+                     uint32_t* __restrict__ OFF2, const int64_t* __restrict__ GB, uint32_t* __restrict__ FILL,
+                     uint32_t* __restrict__ S, uint32_t* __restrict__ gate) {
+    if (*gate == 0) return;
     extern __shared__ __align__(16) uint32_t s_key[];  // [cap_a]
     __shared__ uint32_t s_cur[kStageMaxNB];
     __shared__ uint16_t s_st[kStageMaxNB + 1];
     __shared__ int64_t s_dst[kStageMaxNB];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    __shared__ int s_over;
     const int tid = threadIdx.x;
     const unsigned t = xcd_tile(blockIdx.x, t8);
     if (t >= n_tiles) return;  // uniform
     const int64_t row0 = (int64_t)t * caps.rpt;
     const int64_t ea = (int64_t)Ap[row0];
     const int64_t ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
-    if (ne > caps.cap_a) return;  // uniform: heavy tile, no runs
+    if (ne > caps.cap_a) {  // uniform: heavy tile, no runs
+        for (int b = tid; b <= nb; b += kBlock) OFFT[(size_t)b * ostride + t] = 0;
+        return;
+    }
     const uint32_t n = (uint32_t)ne;
     const int32_t* __restrict__ Ajt = Aj + ea;
     int32_t jj[kMaxE];
@@ -1104,14 +1067,35 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
         const uint32_t e = tid + i * kBlock;
         jj[i] = e < n ? Ajt[e] : -1;
     }
-    const size_t gb = (size_t)(t / kRunGroup) * nb;
+    if (tid < nb) s_cur[tid] = 0;
+    if (tid == 0) s_over = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kMaxE; ++i)
+        if (jj[i] >= 0) atomicAdd(&s_cur[(uint32_t)jj[i] >> sb], 1u);
+    __syncthreads();
+    const uint32_t cnt = tid < nb ? s_cur[tid] : 0u;
+    uint32_t tot;
+    const uint32_t st = block_excl_scan(cnt, s_wsum, &tot);
+    const unsigned sg = (t / kRunGroup) * (unsigned)nb + (unsigned)tid;
+    // claim the runs now; the claims (and the segment bounds) are consumed after the ranking below,
+    // which runs in their shadow
+    uint32_t run = 0;
+    int64_t lo = 0, hi = 0;
+    if (tid < nb && cnt > 0) {
+        run = atomicAdd(&FILL[sg], cnt);
+        lo = GB[sg];
+        hi = GB[sg + 1];
+    }
     if (tid < nb) {
-        const uint32_t st = OFFT[(size_t)tid * ostride + t];
+        OFFT[(size_t)tid * ostride + t] = (uint16_t)st;
         s_st[tid] = (uint16_t)st;
         s_cur[tid] = st;
-        s_dst[tid] = GB[gb + tid] + (int64_t)OFF2[(size_t)tid * ostride + t] - (int64_t)st;
     }
-    if (tid == 0) s_st[nb] = (uint16_t)n;
+    if (tid == 0) {
+        OFFT[(size_t)nb * ostride + t] = (uint16_t)n;
+        s_st[nb] = (uint16_t)n;
+    }
     __syncthreads();
     const uint32_t mask = (1u << sb) - 1u;
 #pragma unroll
@@ -1120,11 +1104,22 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
             const uint32_t pos = atomicAdd(&s_cur[(uint32_t)jj[i] >> sb], 1u);
             s_key[pos] = ((tid + i * kBlock) << 20) | ((uint32_t)jj[i] & mask);
         }
+    if (tid < nb) {
+        if (cnt > 0) {
+            if (lo + run + cnt > hi) s_over = 1;
+            s_dst[tid] = lo + (int64_t)run - (int64_t)st;
+        }
+        OFF2[(size_t)tid * ostride + t] = run;
+    }
     __syncthreads();
+    if (s_over) {  // uniform: a segment's reserve is exceeded
+        if (tid == 0) *gate = 0;
+        return;
+    }
     for (uint32_t q = tid; q < n; q += kBlock) S[s_dst[run_of(s_st, nb, q)] + q] = s_key[q];
 }
 
-// K5: filtered gather, one workgroup per (bucket b, group g) segment, on XCD b % 8 (workgroup i
+// K3: filtered gather, one workgroup per (bucket b, group g) segment, on XCD b % 8 (workgroup i
 // runs on XCD i % 8, so one XCD's CUs work on one bucket at a time and its L2 holds that W32
 // slice). The bucket's nonempty-feature bitmap (2^sb bits) is staged in LDS: an entry whose R row
 // is empty (57% of KDD2012 entries) gets D = 0 without an L2 request, the others gather their
@@ -1132,15 +1127,15 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
 constexpr int kGBlock = 512;  // 8 waves share one staged bitmap (64 KB at 2^19 features)
 __global__ void __launch_bounds__(kGBlock)
 lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__ BM, const int64_t* __restrict__ GB,
-                  int sb, int nb, unsigned groups, const uint32_t* __restrict__ S, uint32_t* __restrict__ D,
-                  const uint32_t* __restrict__ gate) {
-    if (gate && *gate == 0) return;
+                  const uint32_t* __restrict__ FILL, int sb, int nb, unsigned groups, const uint32_t* __restrict__ S,
+                  uint32_t* __restrict__ D, const uint32_t* __restrict__ gate) {
+    if (*gate == 0) return;
     extern __shared__ __align__(16) uint32_t s_bm[];  // 2^sb bits
     const unsigned xcd = blockIdx.x & 7u, k = blockIdx.x >> 3;
     const unsigned b = xcd + 8u * (k / groups);
     if (b >= (unsigned)nb) return;  // uniform
     const unsigned g = k % groups;
-    const int64_t lo = GB[(size_t)g * nb + b], hi = GB[(size_t)g * nb + b + 1];
+    const int64_t lo = GB[(size_t)g * nb + b], hi = lo + FILL[(size_t)g * nb + b];
     if (lo == hi) return;
     const uint32_t nwords = 1u << (sb - 5);
     const uint4* src = reinterpret_cast<const uint4*>(BM + ((size_t)b << (sb - 5)));
@@ -2556,7 +2551,8 @@ struct Plan {
     size_t zero = 0;          // bytes zeroed once per call (header + states [+ carry])
     int64_t scan_blocks = 0;
     size_t lcnt = 0, loff = 0, lhl = 0, ltf = 0, lrow = 0, lcols = 0, lvals = 0;
-    size_t off2 = 0, gb = 0;  // staged runs (lpr_partition_kernel)
+    size_t off2 = 0, gb = 0, fill = 0;  // staged runs (lpr_reserve_kernel, lpr_partition_kernel)
+    int64_t sd_words = 0;               // S / D capacity (words)
     unsigned groups = 0;
 };
 
@@ -2645,10 +2641,15 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
                 pl.offt = pl.total;
                 pl.off2 = pl.offt + al(2 * (size_t)(pl.nb + 1) * pl.ostride);
                 pl.gb = pl.off2 + al(4 * (size_t)pl.nb * pl.ostride);
+                const size_t nseg = (size_t)pl.groups * pl.nb;
+                pl.fill = pl.gb + al(8 * (nseg + 1));
                 // staged entries of one chunk: all of them, or (several chunks) at most cap_a per
-                // tile (a tile past the cap stages nothing)
-                const size_t sd = pl.lpr_chunk < n_rows ? (size_t)pl.n_tiles * (size_t)pl.caps.cap_a : (size_t)nnz_a;
-                pl.s = pl.gb + al(8 * ((size_t)pl.groups * pl.nb + 1));
+                // tile (a tile past the cap stages nothing); plus the segments' reserves
+                // (lpr_reserve_kernel: sum of 8 sqrt(E_s) <= 8 sqrt(segments x entries), 256 each)
+                const double se = pl.lpr_chunk < n_rows ? (double)pl.n_tiles * (double)pl.caps.cap_a : (double)nnz_a;
+                const size_t sd = (size_t)(se + 8.0 * std::sqrt((double)nseg * se)) + 256 * nseg + 1024;
+                pl.sd_words = (int64_t)sd;
+                pl.s = pl.fill + al(4 * nseg);
                 pl.d = pl.s + al(4 * sd);
                 pl.total = pl.d + al(4 * sd);
             }
@@ -2770,37 +2771,35 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
     const IP* Ap = (const IP*)a->indptr;
     const T* Ax = (const T*)a->data;
     const unsigned t8 = (n_tiles + 7) / 8;
-    uint32_t* gate = pl.gated ? reinterpret_cast<uint32_t*>(base + pl.carry + 16) : nullptr;
+    // staged: the gate word says whether this call's staged kernels run (lpr_choose_kernel in auto
+    // mode, 1 when staging is forced); a segment overflow in the partition clears it, and the direct
+    // kernel then takes the rest of the call
+    uint32_t* gate = pl.staged ? reinterpret_cast<uint32_t*>(base + pl.carry + 16) : nullptr;
     LprStage stg{};
     stg.gate = gate;
     if (pl.staged) {
         uint16_t* OFFT = reinterpret_cast<uint16_t*>(base + pl.offt);
         uint32_t* OFF2 = reinterpret_cast<uint32_t*>(base + pl.off2);
         int64_t* GB = reinterpret_cast<int64_t*>(base + pl.gb);
+        uint32_t* FILL = reinterpret_cast<uint32_t*>(base + pl.fill);
         uint32_t* Sw = reinterpret_cast<uint32_t*>(base + pl.s);
         uint32_t* Dw = reinterpret_cast<uint32_t*>(base + pl.d);
-        hipLaunchKernelGGL((lpr_count_kernel<IP>), dim3(8 * t8), dim3(kBlock), 0, st, Ap, a->indices, a->n_rows,
-                           pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, OFFT, gate);
-        HIP_TRY(hipGetLastError());
-        const unsigned nseg = pl.groups * (unsigned)pl.nb;
-        hipLaunchKernelGGL(lpr_run_scan_kernel, dim3(nseg), dim3(kBlock), 0, st, (const uint16_t*)OFFT, OFF2, GB,
-                           n_tiles, pl.nb, pl.ostride, gate);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(lpr_seg_scan_kernel, dim3(1), dim3(1024), 0, st, GB, nseg, gate);
+        hipLaunchKernelGGL((lpr_reserve_kernel<IP>), dim3(1), dim3(kResBlock), 0, st, Ap, a->n_rows, (int)kLprRows,
+                           (int64_t)h->m, pl.groups, pl.sb, pl.nb, pl.sd_words, GB, FILL, gate);
         HIP_TRY(hipGetLastError());
         const size_t plds = 4 * (size_t)pl.caps.cap_a;
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_partition_kernel<IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)plds));
         hipLaunchKernelGGL((lpr_partition_kernel<IP>), dim3(8 * t8), dim3(kBlock), plds, st, Ap, a->indices,
-                           a->n_rows, pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, (const uint16_t*)OFFT,
-                           (const uint32_t*)OFF2, (const int64_t*)GB, Sw, gate);
+                           a->n_rows, pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, OFFT, OFF2,
+                           (const int64_t*)GB, FILL, Sw, gate);
         HIP_TRY(hipGetLastError());
         const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * pl.groups;
         const size_t glds = (size_t)4 << (pl.sb - 5);
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_gather_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)glds));
         hipLaunchKernelGGL(lpr_gather_kernel, dim3(grid), dim3(kGBlock), glds, st, (const uint32_t*)h->W32.p,
-                           (const uint32_t*)h->BM.p, (const int64_t*)GB, pl.sb, pl.nb, pl.groups,
-                           (const uint32_t*)Sw, Dw, gate);
+                           (const uint32_t*)h->BM.p, (const int64_t*)GB, (const uint32_t*)FILL, pl.sb, pl.nb,
+                           pl.groups, (const uint32_t*)Sw, Dw, gate);
         HIP_TRY(hipGetLastError());
         stg = LprStage{gate, nullptr, OFFT, OFF2, GB, Sw, Dw, pl.ostride, pl.nb};
     }
@@ -2822,7 +2821,7 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
         hipLaunchKernelGGL((lpr_main_kernel<T, IP, true>), dim3(grid_for(fn)), dim3(kLprRows), lds, st, R, mag,
                            a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
     }
-    if (!pl.staged || pl.gated) {  // direct gathers (gated: runs iff the device chose them)
+    {  // direct gathers (staged: runs iff the gate is 0 — the device chose them, or a segment overflowed)
         stg.w32 = (const uint32_t*)h->W32.p;
         const void* fn = (const void*)lpr_main_flat_kernel<T, IP, false>;
         HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2862,10 +2861,13 @@ template <typename T, typename IP, typename OP, typename OI>
 int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
                Workspace* ws, const Plan& pl, hipStream_t st) {
     const int64_t n = a->n_rows, step = std::max<int64_t>(pl.lpr_chunk, 1);
+    uint32_t* gate = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + pl.carry + 16);
     if (pl.gated && n > 0) {  // staged or direct for this call, decided on the device (K0)
         hipLaunchKernelGGL((lpr_choose_kernel<IP>), dim3(1), dim3(1024), 0, st, (const IP*)a->indptr, a->indices, n,
-                           reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + pl.carry + 16));
+                           gate);
         HIP_TRY(hipGetLastError());
+    } else if (pl.staged) {  // staging forced: on unless a segment overflows
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)gate, 1u, 1, st));
     }
     int64_t k = 0;
     for (int64_t r0 = 0; r0 < n; r0 += step, ++k) {
@@ -3023,8 +3025,9 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
         rc = dispatch_idx<float, GenericR<float>>(R, 0.0f, h, a, c, order, ws, n_tiles, plan, lds, st);
     }
     if (rc) return rc;
-    // what ran, for rp_project_choice: the device's gate when it decided, else the plan's staging
-    if (plan.lpr && plan.gated)
+    // what ran, for rp_project_choice: the row-lane gate when staged (the device's choice, or a
+    // segment overflow that sent the call to the direct kernel), else the plan's staging
+    if (plan.lpr && plan.staged)
         HIP_TRY(hipMemcpyAsync(&ws->staged_used, reinterpret_cast<char*>(ws) + plan.carry + 16, 4,
                                hipMemcpyDeviceToDevice, st));
     else

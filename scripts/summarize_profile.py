@@ -25,7 +25,7 @@ import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel", "stage_partition_kernel", "stage_gather_kernel",
-                "lpr_count_kernel", "lpr_run_scan_kernel", "lpr_seg_scan_kernel", "lpr_partition_kernel",
+                "lpr_count_kernel", "lpr_run_scan_kernel", "lpr_seg_scan_kernel", "lpr_reserve_kernel", "lpr_partition_kernel",
                 "lpr_gather_kernel", "lpr_main_kernel", "lpr_main_flat_kernel", "lpr_choose_kernel",
                 "lpr_heavy_count_kernel", "lpr_scan_kernel",
                 "lpr_copy_kernel", "lpr_heavy_write_kernel")

@@ -271,7 +271,12 @@ def _rows(rng, k, pool, m, dtype=np.float32):
                           np.concatenate([[0], np.cumsum(k)])), shape=(n, m))
 
 
-def _check_rowlane_staged(R, A, shift):
+def _check_rowlane_staged(R, A, shift, staged=True):
+    """Row-lane pipeline with staging forced on: host path in both orders against the oracle, then
+    the device path, whose workspace records whether the staged gather ran (`staged`) or a segment
+    past its reserve sent the call to the direct kernel."""
+    import torch
+
     want = oracle_product(A, R)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     P = Projector(R)
@@ -280,6 +285,19 @@ def _check_rowlane_staged(R, A, shift):
     assert P.plan(A.shape[0], A.nnz) == {"pipeline": "rowlane", "staged": True, "bucket_shift": shift}
     assert_same_csr(P.matmul(A), *want)
     assert_same_csr(P.matmul(A, order="sorted"), want[0], Cj, Cx)
+    dev = torch.device("cuda", 0)
+    n, nnz = A.shape[0], int(want[0][-1])
+    Ap = torch.as_tensor(A.indptr.astype(np.int32), device=dev)
+    Aj = torch.as_tensor(A.indices.astype(np.int32), device=dev)
+    Ax = torch.as_tensor(A.data, device=dev)
+    ws = torch.empty(P.workspace_bytes(n, A.nnz), dtype=torch.uint8, device=dev)
+    Cp_d = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    Cj_d = torch.empty(nnz + 64, dtype=torch.int32, device=dev)
+    Cx_d = torch.empty(nnz + 64, dtype=torch.float32, device=dev)
+    assert P.project_device(Ap, Aj, Ax, Cp_d, Cj_d, Cx_d, workspace=ws, nnz_a=A.nnz) == nnz
+    assert P.choice(n, A.nnz, ws) == staged
+    got = sp.csr_matrix((Cx_d[:nnz].cpu().numpy(), Cj_d[:nnz].cpu().numpy(), Cp_d.cpu().numpy()), shape=(n, R.shape[1]))
+    assert_same_csr(got, *want)
     P.close()
 
 
@@ -298,33 +316,36 @@ def test_rowlane_staged_tile_of_3200_live_entries(R2m_p1k):
     _check_rowlane_staged(R, A, 16)
 
 
-def test_rowlane_staged_dead_tiles_and_shared_run_starts(R2m_p1k):
+def test_rowlane_staged_dead_tiles_and_empty_rows(R2m_p1k):
     """Tiles none of whose entries has a nonempty R row (every staged word filtered by the gather's
-    bitmap, no products), and a bucket touched only by the first and the last of ~1500 tiles: every
-    tile between has an empty run there, all with the same start in the segment. Plus empty rows."""
+    bitmap, no products) among ~1500 tiles of uniform columns over 245 buckets, plus empty rows: the
+    segment reserves hold (binomial counts), the staged gather runs."""
     rng = np.random.default_rng(1500)
     R = R2m_p1k
     m = R.shape[0]
-    nzr = np.diff(R.indptr) > 0
-    shift = 13
-    b0 = np.arange(0, 1 << shift)
-    live0, dead = b0[nzr[b0]], np.flatnonzero(~nzr)
-    b1 = np.arange(1 << shift, 2 << shift)
-    live1 = b1[nzr[b1]]
-    n_tiles = 1500
-    edge = [(_rows(rng, np.full(256, 2), live0, m) + _rows(rng, np.full(256, 1), live1, m)).tocsr() for _ in range(2)]
-    A = sp.vstack([edge[0], _rows(rng, np.full(256 * 600, 3), live0, m), _rows(rng, np.full(3 * 256, 4), dead, m),
-                   sp.csr_matrix((300, m), dtype=np.float32), _rows(rng, np.full(256 * (n_tiles - 600), 3), live0, m),
-                   edge[1]]).tocsr()
-    A.sort_indices()
-    _check_rowlane_staged(R, A, shift)
+    dead = np.flatnonzero(np.diff(R.indptr) == 0)
+    A = sp.vstack([_rows(rng, np.full(256 * 600, 3), np.arange(m), m), _rows(rng, np.full(3 * 256, 4), dead, m),
+                   sp.csr_matrix((300, m), dtype=np.float32), _rows(rng, np.full(256 * 900, 3), np.arange(m), m)]).tocsr()
+    _check_rowlane_staged(R, A, 13)
+
+
+def test_rowlane_staged_segment_overflow_goes_direct(R2m_p1k):
+    """Staging forced on columns far from uniform (every entry in the first two of 245 buckets):
+    the first tiles' runs exceed their segments' reserves, the partition clears the gate and the
+    direct kernel projects the call; the output is the oracle's either way."""
+    rng = np.random.default_rng(245)
+    R = R2m_p1k
+    m = R.shape[0]
+    A = _rows(rng, np.full(256 * 300, 5), np.arange(2 << 13), m)
+    _check_rowlane_staged(R, A, 13, staged=False)
 
 
 @pytest.mark.parametrize("dist", ["uniform", "powerlaw"])
 def test_auto_staging_choice_on_device(dist):
     """Auto mode on a launch large enough to stage (>= 4M entries, R's W table >= 64 MB): the device
     samples the feature ids and picks the staged gather for uniform columns, direct gathers for
-    power-law ones; either way the whole output equals the forced pipelines' and the oracle's."""
+    power-law ones; staging forced on power-law columns overflows the hot features' segment
+    reserves and goes direct too. Either way the whole output equals the oracle's."""
     import torch
     from randomprojection_amd import synth
 
@@ -345,7 +366,7 @@ def test_auto_staging_choice_on_device(dist):
         Cx = torch.empty(cap, dtype=torch.float32, device="cuda")
         k = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, workspace=ws, nnz_a=nnz_a)
         # what ran is recorded in the workspace by every call, forced modes included
-        assert P.choice(n, nnz_a, ws) == {"auto": dist == "uniform", "on": True, "off": False}[mode]
+        assert P.choice(n, nnz_a, ws) == {"auto": dist == "uniform", "on": dist == "uniform", "off": False}[mode]
         outs[mode] = (Cp.cpu().numpy(), Cj[:k].cpu().numpy(), Cx[:k].cpu().numpy())
         P.close()
     A = sp.csr_matrix((Ax.cpu().numpy(), Aj.cpu().numpy(), Ap.cpu().numpy()), shape=(n, m))
