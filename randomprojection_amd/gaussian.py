@@ -12,9 +12,11 @@ This module streams X through the GPU in row chunks and runs librp's hand-writte
   * "fp64": f64 inputs, v_mfma_f64_16x16x4_f64 with f64 accumulation (sklearn computes in X's dtype);
   * "bf16": inputs rounded to bf16, f32 accumulation (2x less HBM, 16x the f32 MFMA rate) —
     documented reduced-precision mode, checked against an fp64 product of the bf16-rounded inputs.
-The kernels are the product path for device-resident X too: bf16 measured 1221 TF against 1325 TF for
-hipBLASLt on the same 131072 x 16384 -> 1024 block (profiles/r03_dense_*); end to end the pass is
-PCIe-bound either way (X does not fit in HBM).
+The kernels are the product path for device-resident X too, a deliberate trade-off (hand-written
+MFMA path, no library GEMM on the shipped path): on the same 131072 x 16384 -> 1024 block the
+four-stage ring kernel measured bf16 1114 TF vs 1302 TF for hipBLASLt (0.86x) and f32 145 vs 154 TF
+(0.94x), f64 58.8 vs 74.9 TF (profiles/r03_dense_*; scripts/bench_dense.py reports both per run).
+End to end the configs[4] pass is PCIe-bound either way (X does not fit in HBM).
 ``components_`` is generated bit-identically to sklearn (``srp_matrix.gaussian_random_matrix``).
 """
 from __future__ import annotations
