@@ -349,14 +349,14 @@ int launch_dense_glds(const void* X, const void* G, float* Y, int64_t n, int64_t
 // LDS rows of 4 chunks; chunk c of row r at c ^ F(r), F(r) = -(r >> 2) & 3, which makes each of
 // ds_read_b128's 16-lane groups hit 16 distinct 16-B bank slots (rows 16 B x 4 apart share banks
 // only across groups).
-template <bool BF16>
+template <bool BF16, int NS = 4>
 __global__ void __launch_bounds__(512)
 dense_ring_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, float* __restrict__ C,
                   int64_t M, int N, int K, int64_t ldc, unsigned m_tiles, unsigned n_tiles) {
-    constexpr int BM = 256, BN = 256, KC = 4, NS = 4;  // KC: 16-B chunks per 64-B row slice
+    constexpr int BM = 256, BN = 256, KC = 4;  // KC: 16-B chunks per 64-B row slice; NS ring buffers
     constexpr int ES = BF16 ? 2 : 4, KT = 64 / ES;     // element size, elements per K-tile
     constexpr int SZ = (BM + BN) * KC;                  // chunks per stage
-    __shared__ uint4 lds[NS * SZ];                      // 4 x 32 KB
+    __shared__ uint4 lds[NS * SZ];                      // NS x 32 KB
     const unsigned bi = blockIdx.x, xcd = bi & 7u, j = bi >> 3;
     const unsigned mt = (j / n_tiles) * 8u + xcd, nt = j % n_tiles;
     if (mt >= m_tiles) return;  // uniform
@@ -388,7 +388,7 @@ dense_ring_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, floa
     };
 #pragma clang diagnostic pop
     auto stage = [&](int kt) {
-        const uint32_t base = lds0 + (uint32_t)((kt & (NS - 1)) * SZ) * 16u;
+        const uint32_t base = lds0 + (uint32_t)((kt % NS) * SZ) * 16u;
 #pragma unroll
         for (int i = 0; i < 2; ++i) dma(ga[i] + (int64_t)kt * 64, base + i * 512 * 16);
 #pragma unroll
@@ -403,12 +403,15 @@ dense_ring_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, floa
     for (int kt = 0; kt < NS - 1 && kt < steps; ++kt) stage(kt);
     for (int kt = 0; kt < steps; ++kt) {
         // K-tile kt landed (this wave's loads; the barrier: everyone's); younger stages stay in flight
-        if (kt + 2 < steps) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (kt + 1 < steps) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        // (4 loads per stage and thread; NS - 2 younger stages at most)
+        const int younger = std::min(NS - 2, steps - 1 - kt);
+        if (younger >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else if (younger == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (younger == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (kt + NS - 1 < steps) stage(kt + NS - 1);  // into the buffer of K-tile kt - 1: all done with it
-        const uint4* sa = lds + (kt & (NS - 1)) * SZ;
+        const uint4* sa = lds + (kt % NS) * SZ;
         const uint4* sb = sa + BM * KC;
         uint4 bfr[4];
 #pragma unroll
@@ -452,13 +455,13 @@ dense_ring_kernel(const void* __restrict__ Av, const void* __restrict__ Bv, floa
         }
 }
 
-template <bool BF16>
+template <bool BF16, int NS = 4>
 int launch_dense_ring(const void* X, const void* G, float* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
                       hipStream_t st) {
     const unsigned m_tiles = (unsigned)((n + 255) / 256), n_tiles = (unsigned)((p + 255) / 256);
     const uint64_t blocks = (uint64_t)((m_tiles + 7) / 8) * 8ull * n_tiles;
     if (blocks >= (1ull << 31)) return fail(RP_ERR_UNSUPPORTED, "too many rows for one launch");
-    hipLaunchKernelGGL((dense_ring_kernel<BF16>), dim3((unsigned)blocks), dim3(512), 0, st, X, G, Y, n, (int)p, (int)m,
+    hipLaunchKernelGGL((dense_ring_kernel<BF16, NS>), dim3((unsigned)blocks), dim3(512), 0, st, X, G, Y, n, (int)p, (int)m,
                        ldy, m_tiles, n_tiles);
     HIP_TRY(hipGetLastError());
     return RP_OK;

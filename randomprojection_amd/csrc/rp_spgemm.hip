@@ -1144,13 +1144,22 @@ lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__
     const uint32_t mask = (1u << sb) - 1u;
     const uint32_t wb = b << sb;
     constexpr int kU = 8;
-    for (int64_t f0 = (lo & ~int64_t(31)) + threadIdx.x; f0 < hi; f0 += kU * kGBlock) {
-        uint32_t v[kU];
+    // S words streamed (non-temporal: keep the slice in L2), the next chunk's in flight while this
+    // chunk's W32 words are gathered
+    auto load = [&](uint32_t (&v)[kU], int64_t f0) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const int64_t f = f0 + u * kGBlock;
-            v[u] = f >= lo && f < hi ? __builtin_nontemporal_load(S + f) : 0u;  // streamed: keep the slice in L2
+            v[u] = f >= lo && f < hi ? __builtin_nontemporal_load(S + f) : 0u;
         }
+    };
+    uint32_t vn[kU];
+    load(vn, (lo & ~int64_t(31)) + threadIdx.x);
+    for (int64_t f0 = (lo & ~int64_t(31)) + threadIdx.x; f0 < hi; f0 += kU * kGBlock) {
+        uint32_t v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[u] = vn[u];
+        load(vn, f0 + kU * kGBlock);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             const uint32_t col = v[u] & mask;
