@@ -155,8 +155,11 @@ int64_t rp_project_workspace_bytes(const rp_projector* h, int64_t n_rows, int64_
 int64_t rp_project_workspace_bytes_for(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t data_type);
 
 /* Staged gather (packed R, m < 2^30): the A entries of each tile are bucketed by feature range and
- * R's descriptors fetched bucket by bucket from an L2-resident slice (three launches instead of one
- * random 128-B line fill per A entry). mode: -1 auto (large launches over a large R), 0 off, 1 on;
+ * R's descriptors fetched bucket by bucket from an L2-resident slice (one partition pass over A
+ * into per-bucket segments with reserves, then one gather, instead of one random 128-B line fill
+ * per A entry). mode: -1 auto (large launches over a large R; the device then stages only inputs
+ * whose sampled feature ids are near uniform), 0 off, 1 on (the row-lane pipeline still goes
+ * direct for the rest of a call whose columns overflow a segment's reserve: far from uniform);
  * bucket_shift: 2^shift features per bucket (0 = auto, 19). Results are identical either way. */
 int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift);
 
@@ -194,9 +197,10 @@ int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_
 
 /* After an rp_project_device call with `workspace` has completed (its stream synchronised by the
  * caller): *staged = 1 if that call used the staged gather, 0 if direct gathers (rp_project_plan's
- * *staged == 2: decided on the device per call, from a sample of the input's feature ids). The
- * call records what actually ran in the workspace header, so a re-planned call (a workspace too
- * small for staging) reads 0. n_rows / nnz_a are unused (kept for the ABI). 4-byte copy. */
+ * *staged == 2: decided on the device per call, from a sample of the input's feature ids; and a
+ * staged row-lane call whose columns overflowed a segment's reserve finishes direct and reads 0).
+ * The call records what actually ran in the workspace header, so a re-planned call (a workspace
+ * too small for staging) reads 0. n_rows / nnz_a are unused (kept for the ABI). 4-byte copy. */
 int rp_project_choice(const rp_projector* h, int64_t n_rows, int64_t nnz_a, const void* workspace,
                       int32_t* staged);
 
