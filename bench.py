@@ -13,6 +13,12 @@ Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
 
     python bench.py [--config kdd|kdd9x|cfg4] [--gpus N] [--steps K] [--warmup W] [--rows R]
                     [--boundary device|host|libsvm]
+
+--gpus N with N > 1 and no WORLD_SIZE in the environment: this process makes no GPU call, starts
+N rank processes of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free
+MASTER_PORT, as torch.distributed.run sets them), relays rank 0's line and exits with the worst
+rank's status. Under torch.distributed.run (WORLD_SIZE set) a --gpus that differs from WORLD_SIZE
+is an error, never a silent 1-GPU line.
 """
 from __future__ import annotations
 
@@ -56,21 +62,42 @@ CONFIGS = {
 }
 
 
+LIB_ID, LIB_CHECKED = None, False  # build id of the loaded librp (keys profiles/*traffic*.json)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def _src_sha16():
-    import hashlib
+def launch_ranks(n: int) -> int:
+    """--gpus N without a launcher: N child processes of this script, one per GPU (this process
+    touches no GPU, so no exec/fork hazard), the torch.distributed.run environment set for each;
+    rank 0's JSON line is relayed on stdout. A failing rank stops the others (their exact PIDs)."""
+    import socket
+    import subprocess
 
-    h = hashlib.sha256()
-    for n in ("rp_spgemm.hip", "rp_common.h"):
-        with open(os.path.join(ROOT, "randomprojection_amd", "csrc", n), "rb") as f:
-            h.update(f.read())
-    return h.hexdigest()[:16]
-
-
-SRC_SHA16 = _src_sha16()  # keys profiles/*traffic*.json to the kernels they were measured on
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+    out0 = procs[0].communicate()[0]
+    rcs = [procs[0].returncode]
+    for q in procs[1:]:
+        if rcs[0] != 0 and q.poll() is None:
+            q.kill()
+        rcs.append(q.wait())
+    for ln in out0.splitlines():
+        print(ln, flush=True)
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        log(f"bench: rank exit codes {rcs}")
+    return bad[0] if bad else 0
 
 
 def step_kernels(plan, staged_run):
@@ -101,7 +128,10 @@ def main():
                     help="kdd: BASELINE configs[1] (default, weak scaling: 119.7M rows per GPU); kdd9x: "
                          "configs[2], 1.08B rows split over the GPUs (strong scaling); cfg4: configs[3], "
                          "200M x 10M power-law rows, exactly 100 nnz/row -> 1024")
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (= ranks) of this node; default WORLD_SIZE or 1 (see the module doc)")
+    ap.add_argument("--lib", default=None, help="A/B timing only: load this librp build instead of the "
+                                                "package's (its build id is reported, the line says so)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=None)
@@ -128,6 +158,13 @@ def main():
     ap.add_argument("--chunk-rows", type=int, default=0, help="--boundary host: rows per chunk (0 = library default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench: --gpus {args.gpus} but WORLD_SIZE={env_world}: refusing to measure a different "
+                 "number of GPUs than asked")
+    args.gpus = int(env_world or 1)
     cfg = CONFIGS[args.config]
     if args.boundary == "libsvm" and args.rows is None:
         args.rows = 20_000_000  # ~5 GB of text in host memory per rank
@@ -141,7 +178,11 @@ def main():
     from randomprojection_amd import Projector, srp_matrix as sm, synth
     from randomprojection_amd import _native as nat
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    nat.load(args.lib)  # the package's librp is checked against the sources on disk (build id)
+    global LIB_ID, LIB_CHECKED
+    LIB_ID, LIB_CHECKED = nat.build_id(), args.lib is None
+
+    world = args.gpus
     rank = int(os.environ.get("RANK", "0"))
     total_rows_cfg = args.rows
     if cfg.get("strong"):  # a fixed total split over the ranks (contiguous shards)
@@ -206,6 +247,14 @@ def main():
     nnz_a = int(Aj.numel())
     log(f"[rank {rank}] A: {args.rows} rows, nnz={nnz_a} ({time.perf_counter() - t0:.1f}s)")
 
+    if world > 1:
+        ranks_seen = dist.get_world_size()
+        if ranks_seen != world:
+            raise RuntimeError(f"process group has {ranks_seen} ranks, --gpus {world}")
+    args.dist_info = {"ranks_seen": dist.get_world_size() if world > 1 else 1,
+                      "backend": dist.get_backend() if world > 1 else None,
+                      "r_broadcast_ms": t_bcast * 1e3, "rehearsal_one_gpu": rehearse}
+    args.r_meta = meta if world > 1 else None
     if args.boundary in ("host", "libsvm"):
         (bench_host if args.boundary == "host" else bench_libsvm)(args, cfg, P, R_host, Ap, Aj, Ax, world, rank, dev)
         if world > 1:
@@ -267,11 +316,7 @@ def main():
     # workspace header (include/rp.h / rp_spgemm.hip Workspace): tiles taken, deferred tiles
     hdr = ws[:24].cpu().numpy().view(np.uint32)
     n_tiles_run, n_deferred = int(hdr[0]), int(hdr[4])
-    t_max = t_wall
-    if world > 1:
-        tt = torch.tensor([t_wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
+    t_max = _allreduce(t_wall, "max", dev)
 
     a = nnz_a / args.rows
     c = nnz_c / args.rows
@@ -279,12 +324,18 @@ def main():
     b_row = algorithmic_bytes_per_row(a, rbar, c)
     achieved = args.rows * b_row / (kernel_ms * 1e-3) / 1e9
 
+    # the timed output, checked after the clock on EVERY rank: a seeded sample of its rows against the
+    # oracle (bit for bit), and CSR well-formedness of its whole result on the device; reduced with min
+    R_all = _r_host(args, R_host)
+    check = verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_all, seed=20261016 + rank)
+    ok_all = {k: _allreduce(1.0 if check[k] else 0.0, "min", dev) == 1.0
+              for k in ("sample_bitexact_vs_oracle", "indptr_ok", "columns_ok")}
+    check = dict(check, **ok_all, ranks_verified=int(_allreduce(1.0 if all(ok_all.values()) else 0.0, "sum", dev)),
+                 scope="every rank checks its own rows; flags are the min over ranks")
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, Ap, Aj, Ax, R_host)
-    # the timed output, checked after the clock: a seeded sample of rows against the oracle (bit for
-    # bit), and CSR well-formedness of the whole result on the device
-    check = verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host) if rank == 0 else None
+    if rank == 0 and not args.no_cpu_baseline:  # host cores, rank 0 only, the other ranks wait
+        cpu = cpu_baseline(args, Ap, Aj, Ax, R_all)
+    _barrier(dev)
 
     # rocprofv3 PMC results of a profiling session of this same workload on THIS build (profiles/):
     # HBM bytes per step and the L2 hit rate of the main kernel. A traffic file applies only when
@@ -297,7 +348,7 @@ def main():
             tj = json.load(open(f))
         except Exception:  # noqa: BLE001
             continue
-        if (tj.get("rows") == args.rows and tj.get("dist") == args.dist and tj.get("src_sha16") == SRC_SHA16
+        if (tj.get("rows") == args.rows and tj.get("dist") == args.dist and tj.get("src_sha16") == LIB_ID
                 and tj.get("pipeline") == plan["pipeline"] and tj.get("staged") == plan["staged"]
                 and tj.get("staged_this_call", staged_run) == staged_run):
             traffic, tj_used = tj.get("hbm_bytes_per_launch"), tj
@@ -335,7 +386,7 @@ def main():
                          "l2_hit_rate_r_gathers": tj_used.get("l2_hit_rate_r_gathers"),
                          "r_gather_kernel": tj_used.get("gather_kernel"),
                          "l2_hit_rate_main_kernel": tj_used.get("l2_hit_rate_main_kernel"),
-                         "pipeline": plan, "librp_src_sha16": SRC_SHA16,
+                         "pipeline": plan, "librp_src_sha16": LIB_ID,
                          "step_kernels": step_kernels(plan, staged_run),
                          "traffic_GBps": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
                          "random_line_ceiling_G_per_s": RANDOM_LINE_CEILING / 1e9,
@@ -344,8 +395,9 @@ def main():
                              (req * 1e9 / RANDOM_LINE_CEILING) if req else None},
             "cpu_baseline": cpu,
             "verified": check,
+            "librp": {"build_id": LIB_ID, "checked_against_sources": LIB_CHECKED, "path": nat.loaded_path()},
+            **args.dist_info,
             "r_setup_s": t_r,
-            "r_broadcast_ms": t_bcast * 1e3,
             "tiles": n_tiles_run, "deferred_tiles": n_deferred, "staged_this_call": staged_run,
         }
         print(json.dumps(out), flush=True)
@@ -385,7 +437,7 @@ class HostArrays:
 
 
 def _allreduce(x: float, op: str, dev) -> float:
-    """max/min of one float over the ranks (gloo rehearsals reduce on the CPU)."""
+    """max/min/sum of one float over the ranks (gloo rehearsals reduce on the CPU)."""
     import torch
     import torch.distributed as dist
 
@@ -393,7 +445,7 @@ def _allreduce(x: float, op: str, dev) -> float:
         return x
     on = dev if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor([x], dtype=torch.float64, device=on)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
+    dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN, "sum": dist.ReduceOp.SUM}[op])
     return float(t.item())
 
 
@@ -407,13 +459,32 @@ def _barrier(dev):
 
 
 def _r_host(args, R_host):
-    """R on the host for the oracle check after the clock: rank 0 has it; other ranks received only
-    the packed device image over the broadcast and regenerate it (sklearn-identical, seeded)."""
+    """R as host CSR on every rank for the oracle check after the clock: rank 0 built it; the other
+    ranks received only the packed device image, so rank 0 broadcasts the CSR arrays once more
+    (after the timed region; over RCCL on the device, gloo rehearsals on the CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return R_host
+    import scipy.sparse as sp
+
+    meta = args.r_meta
+    on = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else "cpu"
+    m, p, nnz = int(meta["m"]), int(meta["p"]), int(meta["nnz"])
+    if R_host is not None:
+        ts = [torch.from_numpy(np.ascontiguousarray(R_host.indptr, dtype=np.int64)).to(on),
+              torch.from_numpy(np.ascontiguousarray(R_host.indices, dtype=np.int32)).to(on),
+              torch.from_numpy(np.ascontiguousarray(R_host.data, dtype=np.float32)).to(on)]
+    else:
+        ts = [torch.empty(m + 1, dtype=torch.int64, device=on), torch.empty(nnz, dtype=torch.int32, device=on),
+              torch.empty(nnz, dtype=torch.float32, device=on)]
+    for t in ts:
+        dist.broadcast(t, src=0)
     if R_host is not None:
         return R_host
-    from randomprojection_amd import srp_matrix as sm
-
-    return sm.projection_operand(sm.sparse_random_matrix(args.p, args.m, random_state=123))
+    ip, ij, ix = (t.cpu().numpy() for t in ts)
+    return sp.csr_matrix((ix, ij, ip), shape=(m, p))
 
 
 def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
@@ -498,6 +569,8 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
             "cpu_baseline": None,
             "verified": {"sample_rows_per_rank": int(rows.size), "sample_bitexact_vs_oracle": bool(same_all),
                          "indptr_ok": bool(ptr_ok)},
+            "librp": {"build_id": LIB_ID, "checked_against_sources": LIB_CHECKED},
+            **args.dist_info,
         }
         print(json.dumps(out_line), flush=True)
     hm.free()
@@ -591,12 +664,14 @@ def bench_libsvm(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
             "cpu_baseline": None,
             "verified": {"sample_lines_per_rank": int(rows.size), "sample_bitexact_vs_oracle": bool(same_all),
                          "oracle": "oracle/libsvm_ref.py (Spark parseLibSVMRecord + Java double) + oracle/smmp.c"},
+            "librp": {"build_id": LIB_ID, "checked_against_sources": LIB_CHECKED},
+            **args.dist_info,
         }
         print(json.dumps(line), flush=True)
     hm.free()
 
 
-def verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host, n_sample=4096):
+def verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host, n_sample=4096, seed=20261016):
     """After the timed region: Cp monotone from 0 to nnz, every column in [0, p), and a seeded
     sample of rows (spread over the whole matrix) equal to the oracle's restatement of scipy's
     csr_matmat, bit for bit (indices in scipy's per-row order, or ascending for --order sorted, and
@@ -610,7 +685,7 @@ def verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host, n_sample=4096):
     ok_ptr = bool(cp[0].item() == 0 and cp[-1].item() == nnz_c and torch.all(cp[1:] >= cp[:-1]).item())
     cj = Cj[:nnz_c]
     ok_cols = bool(nnz_c == 0 or (int(cj.min().item()) >= 0 and int(cj.max().item()) < args.p))
-    rng = np.random.default_rng(20261016)
+    rng = np.random.default_rng(seed)
     rows = np.sort(rng.choice(args.rows, size=min(n_sample, args.rows), replace=False))
     r_t = torch.as_tensor(rows, device=Ap.device)
     s0, s1 = Ap[r_t].to(torch.int64).cpu().numpy(), Ap[r_t + 1].to(torch.int64).cpu().numpy()

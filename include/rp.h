@@ -122,6 +122,9 @@ typedef struct {
 
 const char* rp_last_error(void);
 const char* rp_version(void);
+/* sha256 prefix (16 hex digits) of the sources the library was built from (build.py); loaders
+ * compare it with the sources on disk and refuse a stale binary. No reference counterpart. */
+const char* rp_build_id(void);
 int rp_device_count(int* count);
 
 int rp_projector_create(int device, int64_t m, int64_t p,

@@ -9,8 +9,6 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "librp.so")
-# timing experiments only (scripts/): RP_LIB names a diagnostic build to load instead
-_LIB_OVERRIDE = os.environ.get("RP_LIB")
 
 RP_OK, RP_ERR_INVALID, RP_ERR_HIP, RP_ERR_CAPACITY, RP_ERR_UNSUPPORTED, RP_ERR_NOMEM, RP_ERR_TIMEOUT = range(7)
 RP_I32, RP_I64, RP_F32, RP_F64, RP_BF16 = 1, 2, 3, 4, 5
@@ -20,7 +18,7 @@ RP_OPT_PIPELINE, RP_OPT_DEFER_POLLS, RP_OPT_DEFER_TICKS, RP_OPT_CHUNK_ROWS, RP_O
 
 # every symbol include/rp.h declares (tests/test_abi.py checks the .so exports them all)
 EXPORTS = (
-    "rp_last_error", "rp_version", "rp_device_count",
+    "rp_last_error", "rp_version", "rp_build_id", "rp_device_count",
     "rp_projector_create", "rp_projector_info_get", "rp_projector_export",
     "rp_projector_create_from_device", "rp_projector_destroy", "rp_pack_r_host",
     "rp_project_workspace_bytes", "rp_project_workspace_bytes_for", "rp_project_plan", "rp_project_choice", "rp_projector_set_staging",
@@ -33,6 +31,10 @@ EXPORTS = (
 
 class NativeUnavailable(RuntimeError):
     pass
+
+
+class StaleLibrary(NativeUnavailable):
+    """librp.so was built from other sources than the ones on disk (build.py source_id)."""
 
 
 class RPError(RuntimeError):
@@ -76,13 +78,45 @@ ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctype
 _lib = None
 
 
-def load(path: str = None):
-    """Load librp.so (built by ``randomprojection_amd.build`` / ``__graft_entry__.build``)."""
-    global _lib
+_lib_path = None
+
+
+def check_build_id(lib, root: str = None) -> str:
+    """The library's source id (rp_build_id) if it equals the id of the sources under ``root``
+    (default: this checkout); else ``StaleLibrary``."""
+    from . import build as _build
+
+    have = lib.rp_build_id().decode()
+    want = _build.source_id(root or _build.ROOT)
+    if have != want:
+        raise StaleLibrary(f"librp was built from sources {have}, the sources on disk are {want}: rebuild it "
+                           "(python -m randomprojection_amd.build); numbers from a stale binary are refused")
+    return have
+
+
+def build_id() -> str:
+    """Source id of the loaded library (checked against the sources when it was loaded)."""
+    return load().rp_build_id().decode()
+
+
+def loaded_path() -> str:
+    load()
+    return _lib_path
+
+
+def load(path: str = None, verify: bool = None):
+    """Load librp.so (built by ``randomprojection_amd.build`` / ``__graft_entry__.build``) and check
+    that it was built from the sources on disk. ``path``: another build (A/B timing scripts only;
+    its id is reported, not checked unless ``verify``)."""
+    global _lib, _lib_path
     if _lib is not None:
+        if path is not None and os.path.abspath(path) != _lib_path:
+            raise NativeUnavailable(f"librp already loaded from {_lib_path}, cannot load {path} too")
         return _lib
+    if verify is None:
+        verify = path is None
     if path is None:
-        path = _LIB_OVERRIDE or LIB_PATH
+        path = LIB_PATH
     if not os.path.exists(path):
         raise NativeUnavailable(
             f"{path} is missing: build it with `python -m randomprojection_amd.build` "
@@ -101,6 +135,7 @@ def load(path: str = None):
     sig = {
         "rp_last_error": (ctypes.c_char_p, []),
         "rp_version": (ctypes.c_char_p, []),
+        "rp_build_id": (ctypes.c_char_p, []),
         "rp_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
         "rp_projector_create": (ctypes.c_int, [ctypes.c_int, i64, i64, vp, i32, vp, i32, vp, i32, i32, P(vp)]),
         "rp_projector_info_get": (ctypes.c_int, [vp, P(ProjectorInfo)]),
@@ -136,13 +171,13 @@ def load(path: str = None):
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name, None)
-        if f is None and path != LIB_PATH:  # an older diagnostic build (RP_LIB, timing scripts only)
-            continue
         if f is None:
             raise NativeUnavailable(f"{path} does not export {name}: rebuild it")
         f.restype = res
         f.argtypes = args
-    _lib = lib
+    if verify:
+        check_build_id(lib)
+    _lib, _lib_path = lib, os.path.abspath(path)
     return lib
 
 

@@ -1,13 +1,26 @@
-"""Build librp.so (HIP, gfx950) in-tree with hipcc. No CUDA, no hipify, no multi-target build."""
+"""Build librp.so (HIP, gfx950) in-tree with hipcc. No CUDA, no hipify, no multi-target build.
+
+Every build embeds the sha256 prefix of its sources (``source_id``) as ``RP_SRC_SHA16``; the
+library returns it from ``rp_build_id()`` and carries it behind a marker in the binary. A build is
+needed exactly when that id differs from the sources on disk (not by file times), and the loader
+(``_native.load``) refuses a library whose id does not match, so no number is ever measured on a
+stale binary under a fresh source hash."""
 from __future__ import annotations
 
 import fcntl
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 SRC = [os.path.join(HERE, "csrc", n) for n in ("rp_spgemm.hip", "rp_libsvm.hip", "rp_dense.hip")]
+# every file the compile reads (relative to the repo root): the id covers all of them
+DEPS = ["randomprojection_amd/csrc/rp_spgemm.hip", "randomprojection_amd/csrc/rp_libsvm.hip",
+        "randomprojection_amd/csrc/rp_dense.hip", "randomprojection_amd/csrc/rp_common.h",
+        "randomprojection_amd/csrc/rp_pow5.h", "include/rp.h"]
 OUT = os.path.join(HERE, "librp.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = [
@@ -15,15 +28,33 @@ FLAGS = [
     # scipy's csr_matmat rounds the multiply and the add separately: never contract to FMA
     "-ffp-contract=off", "-fno-fast-math", "-Wall",
 ]
+MARKER = b"rp-src-sha16:"
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = SRC + [os.path.join(HERE, "..", "include", "rp.h"), os.path.join(HERE, "csrc", "rp_common.h"),
-                  os.path.join(HERE, "csrc", "rp_pow5.h")]
-    return any(os.path.getmtime(s) > t for s in deps)
+def source_id(root: str = ROOT) -> str:
+    """sha256 prefix over (path, contents) of every source file of librp under ``root``."""
+    h = hashlib.sha256()
+    for rel in DEPS:
+        h.update(rel.encode() + b"\0")
+        with open(os.path.join(root, rel), "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def library_id(path: str = OUT) -> str | None:
+    """The source id a built library carries (read from the binary, without loading it)."""
+    try:
+        with open(path, "rb") as f:
+            blob = f.read()
+    except OSError:
+        return None
+    m = re.search(re.escape(MARKER) + rb"([0-9a-f]{16}|unknown)\0", blob)
+    return m.group(1).decode() if m else None
+
+
+def needs_build(out: str = OUT) -> bool:
+    return library_id(out) != source_id()
 
 
 DIAG_OUT = os.path.join(HERE, "librp_diag.so")
@@ -38,13 +69,14 @@ def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str
     # one build at a time (two importers racing on the same objects); re-check under the lock
     with open(os.path.join(HERE, "build", ".lock"), "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
-        if force or diag or needs_build():
+        if force or needs_build(out):
             _compile_and_link(out, diag, verbose)
     return out
 
 
 def _compile_and_link(out: str, diag: bool, verbose: bool) -> None:
-    extra = ["-DRP_STAMPS"] if diag else []
+    sid = source_id()
+    extra = [f'-DRP_SRC_SHA16="{sid}"'] + (["-DRP_STAMPS"] if diag else [])
     odir = os.path.join(HERE, "build", "diag" if diag else "rel")
     os.makedirs(odir, exist_ok=True)
     objs, procs = [], []
@@ -62,6 +94,8 @@ def _compile_and_link(out: str, diag: bool, verbose: bool) -> None:
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+    if library_id(out + ".tmp") != sid:
+        raise RuntimeError(f"{out}.tmp does not carry source id {sid}")
     os.replace(out + ".tmp", out)
 
 

@@ -982,7 +982,7 @@ constexpr int kResBlock = 1024;
 template <typename IP>
 __global__ void __launch_bounds__(kResBlock)
 lpr_reserve_kernel(const IP* __restrict__ Ap, int64_t n_rows, int rpt, int64_t m, unsigned groups, int sb, int nb,
-                   int64_t cap_words, int64_t* __restrict__ GB, uint32_t* __restrict__ FILL,
+                   int cap_a, int64_t cap_words, int64_t* __restrict__ GB, uint32_t* __restrict__ FILL,
                    uint32_t* __restrict__ gate) {
     if (*gate == 0) return;  // the device chose direct gathers for this call
     __shared__ int64_t s[kResBlock];
@@ -992,7 +992,10 @@ lpr_reserve_kernel(const IP* __restrict__ Ap, int64_t n_rows, int rpt, int64_t m
         const unsigned g = sg / (unsigned)nb, b = sg % (unsigned)nb;
         const int64_t r0 = std::min<int64_t>((int64_t)g * kRunGroup * rpt, n_rows);
         const int64_t r1 = std::min<int64_t>((int64_t)(g + 1) * kRunGroup * rpt, n_rows);
-        const double ents = (double)((int64_t)Ap[r1] - (int64_t)Ap[r0]);
+        // a tile past cap_a stages nothing, so a group stages at most cap_a entries per tile (the
+        // workspace's S/D words are sized with the same bound for chunked launches)
+        const double ents = (double)std::min<int64_t>((int64_t)Ap[r1] - (int64_t)Ap[r0],
+                                                      (int64_t)cap_a * ((r1 - r0 + rpt - 1) / rpt));
         const double width = (double)std::min<int64_t>((int64_t)1 << sb, m - ((int64_t)b << sb));
         const double e = ents * width / (double)m;
         return (int64_t)(e + 8.0 * sqrt(e)) + 256;
@@ -1042,14 +1045,20 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
                      unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT,
                      uint32_t* __restrict__ OFF2, const int64_t* __restrict__ GB, uint32_t* __restrict__ FILL,
                      uint32_t* __restrict__ S, uint32_t* __restrict__ gate) {
-    if (*gate == 0) return;
     extern __shared__ __align__(16) uint32_t s_key[];  // [cap_a]
     __shared__ uint32_t s_cur[kStageMaxNB];
     __shared__ uint16_t s_st[kStageMaxNB + 1];
     __shared__ int64_t s_dst[kStageMaxNB];
     __shared__ uint32_t s_wsum[kBlock / 64];
     __shared__ int s_over;
+    __shared__ uint32_t s_gate;
     const int tid = threadIdx.x;
+    // Another workgroup of this launch may clear the gate (segment overflow below) at any time, so
+    // the gate is read ONCE per workgroup and broadcast: every wave takes the same branch (a split
+    // workgroup would run the scan and the S stores with LDS state its exited waves never wrote).
+    if (tid == 0) s_gate = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_gate == 0) return;  // uniform
     const unsigned t = xcd_tile(blockIdx.x, t8);
     if (t >= n_tiles) return;  // uniform
     const int64_t row0 = (int64_t)t * caps.rpt;
@@ -2794,7 +2803,7 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
         uint32_t* Sw = reinterpret_cast<uint32_t*>(base + pl.s);
         uint32_t* Dw = reinterpret_cast<uint32_t*>(base + pl.d);
         hipLaunchKernelGGL((lpr_reserve_kernel<IP>), dim3(1), dim3(kResBlock), 0, st, Ap, a->n_rows, (int)kLprRows,
-                           (int64_t)h->m, pl.groups, pl.sb, pl.nb, pl.sd_words, GB, FILL, gate);
+                           (int64_t)h->m, pl.groups, pl.sb, pl.nb, pl.caps.cap_a, pl.sd_words, GB, FILL, gate);
         HIP_TRY(hipGetLastError());
         const size_t plds = 4 * (size_t)pl.caps.cap_a;
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_partition_kernel<IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -3170,6 +3179,15 @@ int rp_debug_stamps(void* dev_buf) {
 
 const char* rp_last_error(void) { return g_err.c_str(); }
 const char* rp_version(void) { return "rp-mi355x 0.1 (gfx950)"; }
+
+// The sha256 prefix of every source this library was compiled from (build.py passes it as
+// RP_SRC_SHA16 and also finds it in the binary through the marker), so a benched or tested number
+// names the binary that produced it and a stale build is refused (build.py / _native.load).
+#ifndef RP_SRC_SHA16
+#define RP_SRC_SHA16 "unknown"
+#endif
+__attribute__((used)) static const char kBuildMarker[] = "rp-src-sha16:" RP_SRC_SHA16;
+const char* rp_build_id(void) { return kBuildMarker + 13; }
 
 int rp_device_count(int* count) {
     if (!count) return fail(RP_ERR_INVALID, "NULL count");

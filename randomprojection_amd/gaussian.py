@@ -86,8 +86,11 @@ def dense_project_device(X, C, out=None, compute: str = "fp32", stream=None, pre
     cur = torch.cuda.current_stream(X.device)
     if stream is None:
         stream = cur.cuda_stream
-    elif stream != cur.cuda_stream:  # the GEMM reads Xc / Cc on another stream: keep them alive for it
+    elif stream != cur.cuda_stream:
+        # the GEMM reads Xc / Cc on another stream: order it after the casts / pads queued on the
+        # current stream (an event wait on the device, no host sync), and keep them alive for it
         ext = torch.cuda.ExternalStream(stream, device=X.device)
+        ext.wait_stream(cur)
         for t in (Xc, Cc):
             t.record_stream(ext)
     code = {"bf16": nat.RP_BF16, "fp32": nat.RP_F32, "fp64": nat.RP_F64}[compute]

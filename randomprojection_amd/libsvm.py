@@ -209,7 +209,18 @@ def project_text_stream(text, projector, order: str = "sorted", chunk_bytes: int
         exp = items * projector.nnz / max(projector.m, 1)
         cap = int(1.05 * exp + 8 * np.sqrt(exp + 1)) + 65536
     else:
-        rows_cap, cap = out[0].size, out[2].size
+        # the native side trusts these sizes: check them against each other before the call
+        labels, ip, ix, dx = out
+        for name, arr, want in (("labels", labels, (np.float64,)), ("indptr", ip, (np.int32, np.int64)),
+                                ("indices", ix, (np.int32, np.int64)), ("data", dx, (np.float32,))):
+            if not isinstance(arr, np.ndarray) or arr.ndim != 1 or arr.dtype not in [np.dtype(w) for w in want] \
+                    or not arr.flags.c_contiguous or not arr.flags.writeable:
+                raise TypeError(f"out {name}: a writeable contiguous 1-D array of {[np.dtype(w).name for w in want]}")
+        if ix.size != dx.size:
+            raise ValueError(f"out indices ({ix.size}) and data ({dx.size}) must have the same length")
+        if ip.size < labels.size + 1:
+            raise ValueError(f"out indptr needs labels.size + 1 = {labels.size + 1} entries, has {ip.size}")
+        rows_cap, cap = labels.size, dx.size
     for _ in range(2):
         if out is None:
             it = np.dtype(out_index_dtype or (np.int32 if cap < 2**31 else np.int64))

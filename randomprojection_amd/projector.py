@@ -310,7 +310,11 @@ class Projector:
         ``dtype`` (the compute type, float32 or float64) sizes the value parts for it, else for
         float64."""
         if dtype is not None and nnz_a >= 0:
-            code = nat.RP_F64 if np.dtype(str(dtype).replace("torch.", "")) == np.float64 else nat.RP_F32
+            # torch dtypes carry .itemsize; numpy dtypes / scalar types / strings go through np.dtype
+            size = getattr(dtype, "itemsize", None)
+            if not isinstance(size, int):
+                size = np.dtype(dtype).itemsize
+            code = nat.RP_F64 if size == 8 else nat.RP_F32
             return int(self._lib.rp_project_workspace_bytes_for(self._h, int(n_rows), int(nnz_a), code))
         return int(self._lib.rp_project_workspace_bytes(self._h, int(n_rows), int(nnz_a)))
 

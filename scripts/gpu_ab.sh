@@ -14,6 +14,6 @@ fi
 i=0
 for lib in $LIBS; do
   i=$((i + 1))
-  RP_LIB=$lib timeout -k 10 ${BENCH_TIMEOUT:-300} python3 bench.py --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline ${ARGS:-} > gpurun_out/ab_$i.json 2> gpurun_out/ab_$i.err || { tail -20 gpurun_out/ab_$i.err; exit 4; }
+  timeout -k 10 ${BENCH_TIMEOUT:-300} python3 bench.py --lib $lib --steps ${STEPS:-5} --warmup 2 --no-cpu-baseline ${ARGS:-} > gpurun_out/ab_$i.json 2> gpurun_out/ab_$i.err || { tail -20 gpurun_out/ab_$i.err; exit 4; }
   python3 -c "import json,sys;d=json.load(open('gpurun_out/ab_$i.json'));print('$lib', round(d['ms_per_step'],3), 'ms', d['verified'].get('sample_bitexact_vs_oracle'), d['config'].get('nnz_out'))"
 done

@@ -39,3 +39,35 @@ def test_invalid_arguments_rejected_before_device_use():
     assert rc == nat.RP_ERR_INVALID and b"bad shape" in lib.rp_last_error()
     rc = lib.rp_projector_create(0, 10, 40000, None, nat.RP_I32, None, nat.RP_I32, None, nat.RP_F32, 0, ctypes.byref(h))
     assert rc in (nat.RP_ERR_INVALID, nat.RP_ERR_UNSUPPORTED)
+
+
+def test_library_build_id_matches_sources():
+    """The loaded librp carries the source id of the files it was compiled from (build.py), and it is
+    the id of the sources on disk: the loader refuses anything else."""
+    from randomprojection_amd import build
+
+    nat.load()
+    assert nat.build_id() == build.source_id() == build.library_id(nat.LIB_PATH)
+    assert not build.needs_build()
+
+
+def test_touched_source_is_a_stale_library(tmp_path):
+    """A .hip file changed after the build makes the library stale: check_build_id raises."""
+    import shutil
+
+    from randomprojection_amd import build
+
+    lib = nat.load()
+    for rel in build.DEPS:
+        dst = tmp_path / rel
+        dst.parent.mkdir(parents=True, exist_ok=True)
+        shutil.copy(os.path.join(ROOT, rel), dst)
+    assert nat.check_build_id(lib, str(tmp_path)) == build.source_id()
+    with open(tmp_path / "randomprojection_amd" / "csrc" / "rp_spgemm.hip", "a") as f:
+        f.write("// touched\n")
+    try:
+        nat.check_build_id(lib, str(tmp_path))
+    except nat.StaleLibrary as e:
+        assert "rebuild" in str(e)
+    else:
+        raise AssertionError("a touched source was not detected")

@@ -119,3 +119,27 @@ def test_bench_host_boundary_two_ranks():
     assert line["n_gpus"] == 2 and line["config"]["boundary"] == "host"
     assert line["verified"]["sample_bitexact_vs_oracle"] and line["verified"]["indptr_ok"]
     assert line["value"] > 0 and not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]
+
+
+def test_bench_gpus_two_launches_two_ranks():
+    """`bench.py --gpus 2` with no launcher starts its own 2 ranks (rehearsed on cuda:0 over gloo on
+    this one-GPU box; the driver's 8-GPU node runs the same code over RCCL): the line reports
+    n_gpus == ranks_seen == 2, every rank's sampled rows are bit-exact against the oracle, and rank
+    0's host CPU baseline is still there at N > 1 (code/clustermode/randomProjection.py:104,107-110)."""
+    import json
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["RP_BENCH_REHEARSE_ONE_GPU"] = "1"
+    bench = os.path.join(os.path.dirname(HERE), "bench.py")
+    r = subprocess.run([sys.executable, bench, "--gpus", "2", "--rows", "2000000", "--m", "3000000", "--steps", "2",
+                        "--warmup", "1", "--cpu-sample-rows", "200000", "--cpu-part-rows", "20000"],
+                       env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks_seen"] == 2 and line["backend"] == "gloo"
+    v = line["verified"]
+    assert v["sample_bitexact_vs_oracle"] and v["indptr_ok"] and v["columns_ok"] and v["ranks_verified"] == 2
+    assert line["cpu_baseline"] and line["cpu_baseline"]["value"] > 0
+    assert line["librp"]["checked_against_sources"] and line["value"] > 0
