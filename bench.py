@@ -104,8 +104,10 @@ def step_kernels(plan, staged_run):
     """The kernels one rp_project_device call runs for this plan (rp_spgemm.hip); in auto mode the
     other branch's kernels are launched too and exit at once."""
     if plan["pipeline"] == "rowlane":
-        ks = ["lpr_main_kernel" if staged_run else "lpr_main_flat_kernel", "lpr_heavy_count_kernel",
-              "lpr_scan_kernel", "lpr_copy_kernel", "lpr_heavy_write_kernel"]
+        main = (["lpr_unsort_kernel", "lpr_wave_kernel"] if plan.get("split", True) else ["lpr_main_kernel"])
+        ks = (main if staged_run else ["lpr_main_flat_kernel"]) + ["lpr_heavy_count_kernel",
+                                                                  "lpr_scan_kernel", "lpr_copy_kernel",
+                                                                  "lpr_heavy_write_kernel"]
         if staged_run:
             ks = ["lpr_reserve_kernel", "lpr_partition_kernel",
                   "lpr_gather_kernel"] + ks
@@ -147,11 +149,17 @@ def main():
     ap.add_argument("--cpu-part-rows", type=int, default=100_000,
                     help="rows per recipe partition (one per core) in the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--boundary", choices=["device", "host", "libsvm"], default="device",
+    ap.add_argument("--part-rows", type=int, default=1_000_000,
+                    help="--boundary partition: rows of the partition handed to the drop-in per step")
+    ap.add_argument("--recipe-sample-rows", type=int, default=50_000,
+                    help="--boundary partition: rows of the same partition run through the recipe (CPU baseline)")
+    ap.add_argument("--boundary", choices=["device", "host", "libsvm", "partition"], default="device",
                     help="device: inputs/outputs resident in HBM (the default line); host: host CSR in -> host "
                          "CSR out through the chunked stream path (rp_project_stream, PCIe-inclusive); libsvm: "
                          "libsvm text in host memory -> GPU parse + projection -> host CSR "
-                         "(rp_libsvm_project_stream; default 20M rows)")
+                         "(rp_libsvm_project_stream; default 20M rows); partition: the reference's own boundary, "
+                         "random_project_mappartitions_function on a partition of Row dicts (SparseVector "
+                         "features) -> (id, label, SparseVector) tuples")
     ap.add_argument("--chunk-bytes", type=int, default=64 << 20, help="--boundary libsvm: text bytes per chunk")
     ap.add_argument("--host-mem", choices=["pageable", "pinned"], default="pinned",
                     help="--boundary host: host arrays in pageable (numpy) or page-locked (rp_host_alloc) memory")
@@ -168,6 +176,8 @@ def main():
     cfg = CONFIGS[args.config]
     if args.boundary == "libsvm" and args.rows is None:
         args.rows = 20_000_000  # ~5 GB of text in host memory per rank
+    if args.boundary == "partition" and args.rows is None:
+        args.rows = args.part_rows
     for k in ("rows", "m", "p", "dist", "cpu_sample_rows"):
         if getattr(args, k) is None:
             setattr(args, k, cfg[k])
@@ -255,8 +265,9 @@ def main():
                       "backend": dist.get_backend() if world > 1 else None,
                       "r_broadcast_ms": t_bcast * 1e3, "rehearsal_one_gpu": rehearse}
     args.r_meta = meta if world > 1 else None
-    if args.boundary in ("host", "libsvm"):
-        (bench_host if args.boundary == "host" else bench_libsvm)(args, cfg, P, R_host, Ap, Aj, Ax, world, rank, dev)
+    if args.boundary in ("host", "libsvm", "partition"):
+        {"host": bench_host, "libsvm": bench_libsvm, "partition": bench_partition}[args.boundary](
+            args, cfg, P, R_host, Ap, Aj, Ax, world, rank, dev)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -669,6 +680,126 @@ def bench_libsvm(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
         }
         print(json.dumps(line), flush=True)
     hm.free()
+
+
+def bench_partition(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
+    """Boundary 0, the reference's own (code/clustermode/randomProjection.py:15-54, SURVEY.md §8(a)
+    a1): ``random_project_mappartitions_function(rows, R)`` on one partition of ``--part-rows``
+    KDD-shaped rows per rank, given as Row-like dicts with SparseVector features (as Spark's
+    mapPartitions hands them over) and R as the recipe passes it (``components_.T`` as CSC f32,
+    clustermode:101). One step = one call, its lazy output consumed row by row the way a writer
+    consumes it (nothing kept). After the clock: where the time goes (each stage timed alone), the
+    recipe restated (oracle/recipe.py) on a sample of the same rows on one core of this host, and
+    sampled output rows against the oracle, bit for bit."""
+    import collections
+
+    import scipy.sparse as sp
+
+    from oracle import smmp
+    from oracle.recipe import recipe_partition
+    from randomprojection_amd import partition as part
+    from randomprojection_amd.linalg import SparseVector
+
+    n = args.rows
+    ap = Ap[: n + 1].to(torch_int64()).cpu().numpy()
+    aj = Aj[: int(ap[-1])].cpu().numpy()
+    ax = Ax[: int(ap[-1])].cpu().numpy().astype(np.float64)  # libsvm values are doubles
+    del Ap, Aj, Ax
+    m, p = P.m, P.p
+    R_all = _r_host(args, R_host)
+    R_csc = sp.csc_matrix(R_all)  # local_rnd_mat = srp.components_.T.astype(np.float32): CSC m x p
+    t0 = time.perf_counter()
+    rows = [{"id": (rank << 40) + i, "label": float(i & 1),
+             "features": SparseVector._trusted(m, aj[ap[i]:ap[i + 1]], ax[ap[i]:ap[i + 1]])} for i in range(n)]
+    log(f"[rank {rank}] partition of {n} Row dicts built ({time.perf_counter() - t0:.1f}s)")
+
+    def step():
+        collections.deque(part.random_project_mappartitions_function(iter(rows), R_csc), maxlen=0)
+
+    for _ in range(max(args.warmup, 1)):  # the first call uploads R (once per R object)
+        step()
+    _barrier(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    t_wall = time.perf_counter() - t0
+    _barrier(dev)
+    dt = _allreduce(t_wall, "max", dev) / args.steps
+    # where the time goes: each stage of the drop-in alone, same partition
+    proj = part.get_projector(R_csc)
+    t = time.perf_counter()
+    ids, labels, has_label, indptr, indices, values, _ = part.assemble_rows(iter(rows))
+    t_asm = time.perf_counter() - t
+    t = time.perf_counter()
+    Cp, Cj, Cx = proj.project_arrays(indptr, indices, values, order="sorted", out_index_dtype=np.int64)
+    t_gpu = time.perf_counter() - t
+    t = time.perf_counter()
+    out = part.random_project_mappartitions_function(iter(rows), R_csc)
+    t_call = time.perf_counter() - t  # assemble + GPU + conversions: the call returns the lazy zip
+    t = time.perf_counter()
+    collections.deque(out, maxlen=0)
+    t_mat = time.perf_counter() - t
+    # the recipe restated on a sample of the same rows, one core (the reference runs one Python
+    # worker per core); R's CSC -> CSR conversion inside its dot is per partition: timed alone
+    ns = min(args.recipe_sample_rows, n)
+    t = time.perf_counter()
+    ref_out = recipe_partition(rows[:ns], R_csc)
+    t_rec = time.perf_counter() - t
+    t = time.perf_counter()
+    sp.csr_matrix(R_csc)
+    t_conv = time.perf_counter() - t
+    rec_us_row = (t_rec - t_conv) / ns * 1e6 + t_conv / n * 1e6
+    # sampled rows of the drop-in's output against the oracle (scipy's kernel restated + sort),
+    # and the recipe's own output on its sample
+    got = list(part.random_project_mappartitions_function(iter(rows), R_csc))
+    rng = np.random.default_rng(20261018 + rank)
+    sel = np.sort(rng.choice(n, size=min(2048, n), replace=False))
+    A = sp.csr_matrix((ax.astype(np.float32), aj, ap), shape=(n, m))[sel]
+    Wp, Wj, Wx, _, _ = smmp.matmat(A, R_all)
+    Wj, Wx = smmp.sorted_rows(Wp, Wj, Wx)
+    same = len(got) == n
+    for k, r in enumerate(sel.tolist()):
+        i_, l_, v_ = got[r]
+        a, b = Wp[k], Wp[k + 1]
+        same &= (i_ == rows[r]["id"] and l_ == rows[r]["label"] and v_.size == p
+                 and np.array_equal(v_.indices, Wj[a:b].astype(np.int32))
+                 and np.array_equal(v_.values, Wx[a:b].astype(np.float64)))
+    same_rec = all(np.array_equal(g[2].indices, q[2].indices) and np.array_equal(g[2].values, q[2].values)
+                   and g[0] == q[0] and g[1] == q[1] for g, q in zip(got[:ns], ref_out))
+    same_all = _allreduce(1.0 if same and same_rec else 0.0, "min", dev) == 1.0
+    del got, ref_out
+    if rank == 0:
+        line = {
+            "metric": "rows/sec projected (whole node), drop-in random_project_mappartitions_function: Row dicts "
+                      "in -> (id, label, SparseVector) tuples out, KDD2012 54.7M->4096 dims",
+            "value": n * world / dt, "unit": "rows/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": dt * 1e3, "us_per_row": dt / n * 1e6, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": cfg["data"].format(dist=args.dist, p=args.p),
+            "config": {"workload": f"boundary 0: one partition of {n} KDD2012-shaped Row dicts per rank (one "
+                                   "Python process per GPU), R = components_.T CSC f32 as the recipe passes it",
+                       "boundary": "partition", "part_rows": n, "parallelism": f"one partition per rank x{world}"},
+            "where_time_goes_ms": {"assemble_rows": t_asm * 1e3, "gpu_project_host_arrays": t_gpu * 1e3,
+                                   "call_returns_lazy_zip": t_call * 1e3,
+                                   "output_rows_materialised_streamed": t_mat * 1e3},
+            "cpu_baseline": {"value": 1e6 / rec_us_row, "unit": "rows/s", "cores": 1, "kind": "port",
+                             "us_per_row": rec_us_row,
+                             "sample": f"the recipe restated (oracle/recipe.py = clustermode:15-54 step for step), "
+                                       f"first {ns} rows of the same partition on one core; its per-call R CSC->CSR "
+                                       f"conversion ({t_conv:.2f} s) charged once per {n}-row partition",
+                             "sample_s": t_rec, "r_conversion_s": t_conv},
+            "speedup_vs_recipe_per_process": rec_us_row / (dt / n * 1e6),
+            "verified": {"sample_rows_per_rank": int(sel.size), "sample_bitexact_vs_oracle": bool(same_all),
+                         "recipe_sample_equal": "included in the flag (first sample rows vs oracle/recipe.py)"},
+            "librp": {"build_id": LIB_ID, "checked_against_sources": LIB_CHECKED},
+            **args.dist_info,
+        }
+        print(json.dumps(line), flush=True)
+
+
+def torch_int64():
+    import torch
+
+    return torch.int64
 
 
 def verify_output(args, Ap, Aj, Ax, Cp, Cj, Cx, nnz_c, R_host, n_sample=4096, seed=20261016):

@@ -21,9 +21,10 @@
  *      -> scipy _sparsetools.csr_matmat_maxnnz + csr_matmat  scipy/sparse/_compressed.py:569-595
  *    Device-resident CSR in, device-resident CSR out, asynchronous on one stream. The call runs one
  *    of two kernel pipelines (rp_project_plan): the row-lane pipeline for short rows over a packed
- *    R (KDD2012; up to 11 kernels: staged-gather count/scan/partition/gather, main, heavy-tile,
- *    scan, copy) or the tile pipeline for long rows / generic R (one look-back kernel + a copy of
- *    deferred tiles). Output equals scipy's bit for bit: same per-row order
+ *    R (KDD2012: staging choice, segment reserves, super-tile partition, filtered gather, unsort,
+ *    wave kernel (or the direct main kernel when the device picks direct gathers), heavy-tile
+ *    count/write, scan, copy) or the tile pipeline for long rows / generic R (one look-back kernel
+ *    + a copy of deferred tiles). Output equals scipy's bit for bit: same per-row order
  *    (RP_ORDER_SCIPY = reverse first-touch) or ascending (RP_ORDER_SORTED = what pyspark's
  *    SparseVector makes of it, code/clustermode/randomProjection.py:49-50), same zero drop, values
  *    computed with the same separately rounded multiply and add.
@@ -177,13 +178,16 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
  *   RP_OPT_CHUNK_ROWS    row-lane rows per launch sequence: 0 default (2^27), else rounded up to
  *                        whole 256-row tiles
  *   RP_OPT_HOST_THREADS  helper threads of the host result download: -1 default (min(4, cores));
- *                        0 or 1 plain copies */
+ *                        0 or 1 plain copies
+ *   RP_OPT_LPR_SPLIT     staged row-lane pipeline: -1 default (split), 1 split = unsort kernel +
+ *                        barrier-free wave kernel, 0 the persistent main kernel */
 typedef enum {
     RP_OPT_PIPELINE = 1,
     RP_OPT_DEFER_POLLS = 2,
     RP_OPT_DEFER_TICKS = 3,
     RP_OPT_CHUNK_ROWS = 4,
-    RP_OPT_HOST_THREADS = 5
+    RP_OPT_HOST_THREADS = 5,
+    RP_OPT_LPR_SPLIT = 6
 } rp_option;
 int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value);
 int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* value);

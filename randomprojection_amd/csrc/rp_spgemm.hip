@@ -458,24 +458,17 @@ __device__ __forceinline__ uint32_t lds_excl_scan(V* a, uint32_t n, uint32_t* s_
     return total;
 }
 
-// Staged mode (STAGED, packed R only): stage 1a reads each entry's R descriptor from the staging
-// buffers written by stage_partition_kernel + stage_gather_kernel (below) instead of gathering it
-// from W: S[q] = entry << 20 | column-in-bucket and D[q] = W32 word of that column, for the tile's
-// entries in bucket order (q relative to Ap[0]). Two coalesced 4-byte reads per entry replace one
-// random 128-B line fill.
 // WPE: minimum waves per SIMD the register allocation must allow (1 = unconstrained: 76 VGPRs,
 // 6 waves). 7 is used when the tile's LDS leaves room for 7 tiles per CU (configs[3]: 29-row tiles,
 // 19.6 KB; f32 packed, 71 VGPRs, no spills): 252 -> 235 ms. KDD2012 tiles (26.9 KB) are
 // LDS-limited to 5 per CU, where the tighter allocation measured 3% slower.
-template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED, int WPE = 1>
+template <typename T, typename IP, typename OP, typename OI, typename RL, int WPE = 1>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WPE)))
 spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict__ Ap,
                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
                        OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
                        unsigned long long capacity, Caps caps, int order, Workspace* ws,
-                       unsigned int n_tiles, const uint32_t* __restrict__ S,
-                       const T* __restrict__ SX, const uint32_t* __restrict__ D,
-                       DeferSpace dfr, int defer_polls, int defer_ticks) {
+                       unsigned int n_tiles, DeferSpace dfr, int defer_polls, int defer_ticks) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ uint16_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative, <= cap_a)
     __shared__ uint16_t s_rowS[kBlock + 1];    // row -> first product
@@ -512,47 +505,22 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     if (nnz_t <= caps.cap_a) {  // uniform
         const uint32_t ne = (uint32_t)nnz_t;
         for (int r = tid; r <= nrows; r += kBlock) s_rowptr[r] = (uint16_t)((int64_t)Ap[row0 + r] - ea);
-        // ---- stage 1a: coalesced A entries, one R-descriptor gather per entry (direct), or the
-        // staged descriptors read in bucket order and scattered to their entries (STAGED).
-        // Registers (kept across the scan below): direct d = the 64-bit W word; staged dw = the
-        // 32-bit W32 word (code 3 = "take W[j]": re-fetched in stage 1c, 2% of KDD2012 entries)
-        // and the entry index, two 16-bit halves per register.
-        constexpr int kD = STAGED ? 1 : kMaxE, kW = STAGED ? kMaxE : 1, kE = STAGED ? kMaxE / 2 : 1;
-        uint64_t d[kD];
-        uint32_t dw[kW];
-        uint32_t eixp[kE];
+        // ---- stage 1a: coalesced A entries, one R-descriptor gather per entry, kept in registers
+        // across the scan below (the 64-bit W word, or a generic R's row start)
+        uint64_t d[kMaxE];
         T x[kMaxE];
-        const int64_t q0 = STAGED ? ea - (int64_t)Ap[0] : 0;
-        const uint32_t* __restrict__ St = S + q0;   // uniform bases: scalar + 32-bit lane offsets
-        const uint32_t* __restrict__ Dt = D + q0;
-        const T* __restrict__ SXt = SX + q0;
         const int32_t* __restrict__ Ajt = Aj + ea;
         const T* __restrict__ Axt = Ax + ea;
 #pragma unroll
         for (int i = 0; i < kMaxE; ++i) {
             const uint32_t e = tid + i * kBlock;
             x[i] = T(0);
-            if constexpr (STAGED) {
-                dw[i] = 0;
-                if ((i & 1) == 0) eixp[i >> 1] = 0;
-            } else {
-                d[i] = 0;
-            }
+            d[i] = 0;
             if (e < ne) {
-                uint32_t cnt, ei = e;
-                if constexpr (STAGED) {
-                    x[i] = SXt[e];
-                    const uint32_t w = Dt[e];
-                    ei = St[e] >> 20;
-                    eixp[i >> 1] |= ei << (16 * (i & 1));
-                    dw[i] = w;
-                    cnt = w >> 30;
-                    if (cnt == 3) (void)r_describe<T>(R, (int32_t)(w & kW32J), cnt);
-                } else {
-                    x[i] = Axt[e];
-                    d[i] = r_describe<T>(R, Ajt[e], cnt);
-                }
-                s_eoff[ei] = (uint16_t)std::min<uint32_t>(cnt, 0xffffu);
+                uint32_t cnt;
+                x[i] = Axt[e];
+                d[i] = r_describe<T>(R, Ajt[e], cnt);
+                s_eoff[e] = (uint16_t)std::min<uint32_t>(cnt, 0xffffu);
             }
         }
         __syncthreads();
@@ -574,18 +542,8 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
 #pragma unroll
             for (int i = 0; i < kMaxE; ++i) {
                 if (tid + i * kBlock < ne) {
-                    uint32_t e;
-                    uint64_t de;
-                    if constexpr (STAGED) {
-                        e = (eixp[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-                        const uint32_t code = dw[i] >> 30;
-                        uint32_t cnt;
-                        de = code == 3 ? r_describe<T>(R, (int32_t)(dw[i] & kW32J), cnt)
-                                       : (((uint64_t)code << 61) | (uint64_t)(dw[i] & 0x3fffffffu));
-                    } else {
-                        e = tid + i * kBlock;
-                        de = d[i];
-                    }
+                    const uint32_t e = tid + i * kBlock;
+                    const uint64_t de = d[i];
                     const uint32_t o0 = s_eoff[e], o1 = s_eoff[e + 1];
                     const uint32_t rtag = (uint32_t)s_erow[e] << 16;
                     for (uint32_t t = 0; t < o1 - o0; ++t) {
@@ -745,21 +703,17 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
 }
 
 // ------------------------------------------------------------------------------------------
-// Staged gather. Uniform columns over a 437 MB W make every descriptor gather a
-// random 128-B line fill, capped near 55 G lines/s on MI355X whatever the load flavour
-// (profiles/r01_probe_gather_*.json). Staging turns them into L2 hits plus streams:
-//   partition (per tile, coalesced): counting-sort the tile's entries by column bucket
-//             (2^sb features = a W32 slice of 4 * 2^sb bytes) into S (tile-major: the tile's
-//             S range is its own A range), bucket starts into OFFT[bucket][tile];
-//   gather    (per bucket, each XCD on its own buckets so the slice stays in that XCD's 4 MB L2):
-//             D[q] = W32[bucket << sb | S[q] & mask] over every tile's run of the bucket;
-//   the main kernel then reads S and D of its tile with coalesced loads.
+// Staged gather of the row-lane pipeline. Uniform columns over a 437 MB W make
+// every descriptor gather a random 128-B line fill, capped near 55 G lines/s on MI355X whatever the
+// load flavour (profiles/r01_probe_gather_*.json). Staging turns them into L2 hits plus streams: the
+// tile's entries are partitioned by column bucket (2^sb features = a W32 slice of 4 * 2^sb bytes),
+// each bucket's words gathered on one XCD whose 4 MB L2 holds the slice, and the descriptors put
+// back into entry order. (The tile pipeline's own staged gather, measured slower than its direct
+// gathers in every configuration, was removed in round 4.)
 // W32 word of feature j (built from W): bits 30-31 = n if the R row has n <= 2 entries, the low
 // 30 bits then hold W's slots 0-1 unchanged; n = 3 marks "more": the low 30 bits are j itself and
 // the main kernel takes the full word from W (2% of KDD2012 features).
-constexpr int kStageTB = 256;     // tiles per gather workgroup (one per thread for the run bounds)
 constexpr int kStageMaxNB = 256;  // buckets (one per thread in the partition scan)
-constexpr int kStageMap = 16384;  // gather: element -> run map entries (u8) in LDS
 
 // bit j of BM = feature j has at least one R entry (57% of KDD2012 features have none)
 __global__ void build_bitmap_kernel(const uint64_t* __restrict__ W, uint32_t* __restrict__ BM, int64_t m) {
@@ -787,153 +741,17 @@ __global__ void build_w32_kernel(const uint64_t* __restrict__ W, const uint16_t*
 }
 
 
-// one workgroup per tile: bucket histogram (LDS atomics), scan, the tile's entries sorted into LDS,
-// then written to S/SX with coalesced stores; bucket starts go to OFFT[b][t] (adjacent tiles'
-// stores merge in L2), the tile's first entry to TE[t].
-template <typename T, typename IP>
-__global__ void __launch_bounds__(kBlock)
-stage_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
-                       const T* __restrict__ Ax, int64_t n_rows, Caps caps, unsigned n_tiles,
-                       int sb, int nb, uint32_t ostride, uint32_t* __restrict__ S,
-                       T* __restrict__ SX, uint16_t* __restrict__ OFFT, int64_t* __restrict__ TE) {
-    extern __shared__ __align__(16) unsigned char lds[];  // sorted keys [cap_a] u32, values [cap_a] T
-    __shared__ uint32_t s_hist[kStageMaxNB];
-    __shared__ uint32_t s_wsum[kBlock / 64];
-    uint32_t* s_key = reinterpret_cast<uint32_t*>(lds);
-    T* s_val = reinterpret_cast<T*>(lds + 4 * (size_t)caps.cap_a);
-    const int tid = threadIdx.x;
-    const unsigned t = blockIdx.x;
-    const int64_t a0 = (int64_t)Ap[0];
-    const int64_t row0 = (int64_t)t * caps.rpt;
-    const int64_t ea = (int64_t)Ap[row0];
-    const int64_t ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
-    if (tid == 0) TE[t] = ea - a0;
-    if (ne > caps.cap_a) {  // the main kernel's exact slow path reads A itself: empty runs
-        for (int b = tid; b <= nb; b += kBlock) OFFT[(size_t)b * ostride + t] = 0;
-        return;
-    }
-    const uint32_t n = (uint32_t)ne;
-    const uint32_t mask = (1u << sb) - 1u;
-    if (tid < nb) s_hist[tid] = 0;
-    __syncthreads();
-    const int32_t* __restrict__ Ajt = Aj + ea;  // uniform bases, 32-bit lane offsets
-    const T* __restrict__ Axt = Ax + ea;
-    int32_t jj[kMaxE];
-    uint32_t rk[kMaxE];
-#pragma unroll
-    for (int i = 0; i < kMaxE; ++i) {
-        const uint32_t e = tid + i * kBlock;
-        if (e < n) {
-            jj[i] = Ajt[e];
-            rk[i] = atomicAdd(&s_hist[(uint32_t)jj[i] >> sb], 1u);
-        }
-    }
-    __syncthreads();
-    uint32_t tot;
-    const uint32_t base = block_excl_scan(tid < nb ? s_hist[tid] : 0u, s_wsum, &tot);
-    if (tid < nb) {
-        s_hist[tid] = base;
-        OFFT[(size_t)tid * ostride + t] = (uint16_t)base;
-    }
-    if (tid == 0) OFFT[(size_t)nb * ostride + t] = (uint16_t)n;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kMaxE; ++i) {
-        const uint32_t e = tid + i * kBlock;
-        if (e < n) {
-            const uint32_t pos = s_hist[(uint32_t)jj[i] >> sb] + rk[i];
-            s_key[pos] = (e << 20) | ((uint32_t)jj[i] & mask);
-            if (SX) s_val[pos] = Axt[e];
-        }
-    }
-    __syncthreads();
-    uint32_t* __restrict__ St = S + (ea - a0);
-    T* __restrict__ SXt = SX ? SX + (ea - a0) : nullptr;
-#pragma unroll
-    for (int i = 0; i < kMaxE; ++i) {
-        const uint32_t e = tid + i * kBlock;
-        if (e < n) {
-            St[e] = s_key[e];
-            if (SX) SXt[e] = s_val[e];
-        }
-    }
-}
-
-// grid: 8 * ceil(nb / 8) * groups workgroups; workgroup i runs on XCD i % 8 (round-robin dispatch),
-// which takes buckets i % 8, i % 8 + 8, ... in turn, `groups` workgroups of kStageTB tiles each.
-__global__ void __launch_bounds__(kBlock)
-stage_gather_kernel(const uint32_t* __restrict__ W32, const int64_t* __restrict__ TE,
-                    unsigned n_tiles, int sb, int nb, uint32_t ostride, unsigned groups,
-                    const uint16_t* __restrict__ OFFT, const uint32_t* __restrict__ S,
-                    uint32_t* __restrict__ D) {
-    extern __shared__ __align__(16) unsigned char lds[];  // run index of every element (u8)
-    __shared__ uint32_t s_scan[kStageTB + 1];
-    __shared__ int64_t s_base[kStageTB];
-    __shared__ uint32_t s_wsum[kBlock / 64];
-    uint8_t* s_run = lds;
-    const int tid = threadIdx.x;
-    const unsigned xcd = blockIdx.x & 7u, k = blockIdx.x >> 3;
-    const unsigned b = xcd + 8u * (k / groups);
-    if (b >= (unsigned)nb) return;  // uniform
-    const unsigned t = (k % groups) * kStageTB + tid;
-    uint32_t len = 0;
-    if (t < n_tiles) {
-        const uint32_t st = OFFT[(size_t)b * ostride + t], en = OFFT[(size_t)(b + 1) * ostride + t];
-        len = en - st;
-        s_base[tid] = TE[t] + st;
-    }
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(len, s_wsum, &total);
-    s_scan[tid] = ex;
-    if (tid == 0) s_scan[kStageTB] = total;
-    // element f of the workgroup belongs to run s_run[f] (an LDS map of the first kStageMap elements)
-    for (uint32_t f = ex; f < std::min<uint32_t>(ex + len, kStageMap); ++f) s_run[f] = (uint8_t)tid;
-    __syncthreads();
-    const uint32_t mask = (1u << sb) - 1u;
-    const uint32_t hi = b << sb;
-    constexpr int kU = 8;  // independent S -> W32 -> D chains in flight per thread
-    for (uint32_t f0 = 0; f0 < total; f0 += kU * kBlock) {
-        int64_t q[kU];
-        uint32_t v[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint32_t f = f0 + u * kBlock + tid;
-            q[u] = -1;
-            if (f < total) {
-                uint32_t r;
-                if (f < kStageMap) {
-                    r = s_run[f];
-                } else {  // past the map (a bucket holding most of 256 tiles' entries): search
-                    uint32_t lo = 0, up = kStageTB;
-                    while (up - lo > 1) {
-                        const uint32_t mid = (lo + up) >> 1;
-                        if (s_scan[mid] <= f) lo = mid; else up = mid;
-                    }
-                    r = lo;
-                }
-                q[u] = s_base[r] + (f - s_scan[r]);
-                v[u] = S[q[u]];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u)
-            if (q[u] >= 0) v[u] = W32[hi | (v[u] & mask)];
-#pragma unroll
-        for (int u = 0; u < kU; ++u)
-            if (q[u] >= 0) D[q[u]] = v[u];
-    }
-}
-
 // ---- staging for the row-lane pipeline: bucket-major runs inside groups of kRunGroup tiles.
 // S holds, for tile group g and bucket b, the entries of all the group's tiles whose feature falls
 // in b as ONE contiguous segment (one run per tile, runs in claim order, rank order inside the
 // run); segments are laid out in (g, b) order, each with a reserve sized from the group's entries
 // (lpr_reserve_kernel). So the gather streams whole segments (full 128-byte lines, nothing shared
 // between workgroups), and a tile's entries come back as nb runs. One pass over A (the partition
-// claims each run with an atomicAdd on its segment's fill); a segment past its reserve (columns far
-// from uniform) sends the call to the direct kernel. Index arrays (workspace):
-//   OFFT[b][t] (u16)  within-tile start of bucket b (bucket order), OFFT[nb][t] = the tile's entries
-//   OFF2[b][t] (u32)  start of tile t's run in segment (g, b), relative to the segment
+// claims the runs of a super-tile of four tiles with one atomicAdd per bucket on its segment's
+// fill); a segment past its reserve (columns far from uniform) sends the call to the direct
+// kernel. Index arrays (workspace, tile-major: a tile's table is contiguous):
+//   OFFT[t][b] (u16)  within-tile start of bucket b (bucket order), OFFT[t][nb] = the tile's entries
+//   OFF2[t][b] (u32)  start of tile t's run in segment (g, b), relative to the segment
 //   GB[g*nb + b] (i64) segment start in S (exclusive prefix of the reserves), FILL[g*nb + b] its fill
 // A tile past the entry cap stages nothing (its counts are 0): the heavy path reads A itself.
 constexpr int kRunGroup = 4096;  // tiles per group (uniform KDD2012: ~110K entries per segment)
@@ -1031,101 +849,124 @@ __device__ __forceinline__ uint32_t run_of(const uint16_t* st, int nb, uint32_t 
     return lo;
 }
 
-// K2: partition, one workgroup per tile: the tile's entries histogrammed by bucket in LDS, the
-// within-tile bucket starts -> OFFT, each nonempty bucket's run claimed in its (group, bucket)
-// segment by one atomicAdd on FILL -> OFF2, the entries ranked into bucket order in LDS and written
-// to their runs (consecutive lanes -> consecutive S words inside a run). S word: entry index in the
-// tile << 20 | column bits. Runs land in a segment in claim order (any order: the main kernel finds
-// a tile's runs through OFF2). A run past its segment's reserve sets the gate to 0: the call's
-// remaining kernels take the direct path (lpr_main_flat_kernel). A tile past the entry cap stages
-// nothing (its counts are 0): the heavy path reads A itself.
+// K2: partition, one workgroup per SUPER-TILE of kPartTiles = 4 consecutive tiles (one 256-thread
+// quarter per tile). Each tile's entries are histogrammed by bucket in LDS, its within-tile bucket
+// starts go to OFFT, and ONE atomicAdd per bucket on FILL claims the (group, bucket) segment room of
+// all four tiles at once: the four runs of a bucket are adjacent in their segment, in tile order
+// (OFF2 = each run's position), so the unsort pass reads a super-tile's runs of a bucket as one
+// contiguous range and the S stores of a bucket fill whole lines inside one workgroup. The entries
+// are ranked into bucket order in LDS and written to their runs (consecutive lanes -> consecutive S
+// words). S word: entry index in the tile << 20 | column bits. A run past its segment's reserve
+// sets the gate to 0: the call's remaining kernels take the direct path (lpr_main_flat_kernel). A
+// tile past the entry cap stages nothing (its counts are 0): the heavy path reads A itself.
+constexpr int kPartTiles = 4;
+constexpr int kPBlock = kBlock * kPartTiles;
+static_assert(kRunGroup % kPartTiles == 0, "a super-tile never straddles two groups");
 template <typename IP>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kPBlock)
 lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, Caps caps,
-                     unsigned n_tiles, unsigned t8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT,
+                     unsigned n_tiles, unsigned s8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT,
                      uint32_t* __restrict__ OFF2, const int64_t* __restrict__ GB, uint32_t* __restrict__ FILL,
                      uint32_t* __restrict__ S, uint32_t* __restrict__ gate) {
-    extern __shared__ __align__(16) uint32_t s_key[];  // [cap_a]
-    __shared__ uint32_t s_cur[kStageMaxNB];
-    __shared__ uint16_t s_st[kStageMaxNB + 1];
-    __shared__ int64_t s_dst[kStageMaxNB];
-    __shared__ uint32_t s_wsum[kBlock / 64];
+    extern __shared__ __align__(16) uint32_t s_key[];  // [kPartTiles][cap_a]
+    __shared__ uint32_t s_cur[kPartTiles][kStageMaxNB];
+    __shared__ uint16_t s_st[kPartTiles][kStageMaxNB + 1];
+    __shared__ int64_t s_dst[kPartTiles][kStageMaxNB];
+    __shared__ uint32_t s_wsum[kPBlock / 64];
     __shared__ int s_over;
     __shared__ uint32_t s_gate;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, q = tid >> 8, qt = tid & (kBlock - 1), w = tid >> 6;
     // Another workgroup of this launch may clear the gate (segment overflow below) at any time, so
     // the gate is read ONCE per workgroup and broadcast: every wave takes the same branch (a split
     // workgroup would run the scan and the S stores with LDS state its exited waves never wrote).
     if (tid == 0) s_gate = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (s_gate == 0) return;  // uniform
-    const unsigned t = xcd_tile(blockIdx.x, t8);
-    if (t >= n_tiles) return;  // uniform
-    const int64_t row0 = (int64_t)t * caps.rpt;
-    const int64_t ea = (int64_t)Ap[row0];
-    const int64_t ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
-    if (ne > caps.cap_a) {  // uniform: heavy tile, no runs
-        for (int b = tid; b <= nb; b += kBlock) OFFT[(size_t)b * ostride + t] = 0;
-        return;
+    const unsigned t0 = xcd_tile(blockIdx.x, s8) * kPartTiles;
+    if (t0 >= n_tiles) return;  // uniform
+    const unsigned t = t0 + q;
+    const bool live = t < n_tiles;  // quarter-uniform
+    int64_t ea = 0, ne = 0;
+    if (live) {
+        const int64_t row0 = (int64_t)t * caps.rpt;
+        ea = (int64_t)Ap[row0];
+        ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
     }
-    const uint32_t n = (uint32_t)ne;
+    const uint32_t n = ne > caps.cap_a ? 0u : (uint32_t)ne;  // a heavy tile stages nothing: all runs empty
     const int32_t* __restrict__ Ajt = Aj + ea;
     int32_t jj[kMaxE];
 #pragma unroll
     for (int i = 0; i < kMaxE; ++i) {
-        const uint32_t e = tid + i * kBlock;
+        const uint32_t e = qt + i * kBlock;
         jj[i] = e < n ? Ajt[e] : -1;
     }
-    if (tid < nb) s_cur[tid] = 0;
+    if (qt < nb) s_cur[q][qt] = 0;
     if (tid == 0) s_over = 0;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kMaxE; ++i)
-        if (jj[i] >= 0) atomicAdd(&s_cur[(uint32_t)jj[i] >> sb], 1u);
+        if (jj[i] >= 0) atomicAdd(&s_cur[q][(uint32_t)jj[i] >> sb], 1u);
     __syncthreads();
-    const uint32_t cnt = tid < nb ? s_cur[tid] : 0u;
-    uint32_t tot;
-    const uint32_t st = block_excl_scan(cnt, s_wsum, &tot);
-    const unsigned sg = (t / kRunGroup) * (unsigned)nb + (unsigned)tid;
-    // claim the runs now; the claims (and the segment bounds) are consumed after the ranking below,
-    // which runs in their shadow
-    uint32_t run = 0;
+    const uint32_t cnt = qt < nb ? s_cur[q][qt] : 0u;
+    // the super-tile's claim of bucket qt (quarter 0): issued now, consumed after the ranking
+    uint32_t claim = 0, c4[kPartTiles] = {};
     int64_t lo = 0, hi = 0;
-    if (tid < nb && cnt > 0) {
-        run = atomicAdd(&FILL[sg], cnt);
-        lo = GB[sg];
-        hi = GB[sg + 1];
+    const unsigned sg = (t0 / kRunGroup) * (unsigned)nb + (unsigned)qt;
+    if (q == 0 && qt < nb) {
+        uint32_t tot4 = 0;
+#pragma unroll
+        for (int k = 0; k < kPartTiles; ++k) {
+            c4[k] = s_cur[k][qt];
+            tot4 += c4[k];
+        }
+        if (tot4 > 0) {
+            claim = atomicAdd(&FILL[sg], tot4);
+            lo = GB[sg];
+            hi = GB[sg + 1];
+        }
     }
-    if (tid < nb) {
-        OFFT[(size_t)tid * ostride + t] = (uint16_t)st;
-        s_st[tid] = (uint16_t)st;
-        s_cur[tid] = st;
+    // within-tile bucket starts: exclusive scan of cnt over the quarter's 256 threads
+    const uint32_t inc = wave_incl_scan(cnt);
+    if ((tid & 63) == 63) s_wsum[w] = inc;
+    __syncthreads();
+    uint32_t st = inc - cnt;
+    for (int i = 4 * q; i < w; ++i) st += s_wsum[i];
+    if (qt < nb) {
+        s_st[q][qt] = (uint16_t)st;
+        s_cur[q][qt] = st;
+        if (live) OFFT[(size_t)t * ostride + qt] = (uint16_t)st;
     }
-    if (tid == 0) {
-        OFFT[(size_t)nb * ostride + t] = (uint16_t)n;
-        s_st[nb] = (uint16_t)n;
+    if (qt == 0) {
+        s_st[q][nb] = (uint16_t)n;
+        if (live) OFFT[(size_t)t * ostride + nb] = (uint16_t)n;
     }
     __syncthreads();
     const uint32_t mask = (1u << sb) - 1u;
+    uint32_t* sk = s_key + (size_t)q * caps.cap_a;
 #pragma unroll
     for (int i = 0; i < kMaxE; ++i)
         if (jj[i] >= 0) {
-            const uint32_t pos = atomicAdd(&s_cur[(uint32_t)jj[i] >> sb], 1u);
-            s_key[pos] = ((tid + i * kBlock) << 20) | ((uint32_t)jj[i] & mask);
+            const uint32_t pos = atomicAdd(&s_cur[q][(uint32_t)jj[i] >> sb], 1u);
+            sk[pos] = ((qt + i * kBlock) << 20) | ((uint32_t)jj[i] & mask);
         }
-    if (tid < nb) {
-        if (cnt > 0) {
-            if (lo + run + cnt > hi) s_over = 1;
-            s_dst[tid] = lo + (int64_t)run - (int64_t)st;
+    if (q == 0 && qt < nb) {  // the four tiles' runs of bucket qt, adjacent in tile order
+        uint32_t run = claim;
+        if (c4[0] + c4[1] + c4[2] + c4[3] > 0 && lo + (int64_t)claim + c4[0] + c4[1] + c4[2] + c4[3] > hi) s_over = 1;
+#pragma unroll
+        for (int k = 0; k < kPartTiles; ++k) {
+            if (t0 + k < n_tiles) {
+                s_dst[k][qt] = lo + (int64_t)run - (int64_t)s_st[k][qt];
+                OFF2[(size_t)(t0 + k) * ostride + qt] = run;
+            }
+            run += c4[k];
         }
-        OFF2[(size_t)tid * ostride + t] = run;
     }
     __syncthreads();
     if (s_over) {  // uniform: a segment's reserve is exceeded
         if (tid == 0) *gate = 0;
         return;
     }
-    for (uint32_t q = tid; q < n; q += kBlock) S[s_dst[run_of(s_st, nb, q)] + q] = s_key[q];
+    for (uint32_t pos = qt; pos < n; pos += kBlock) S[s_dst[q][run_of(s_st[q], nb, pos)] + pos] = sk[pos];
 }
 
 // K3: filtered gather, one workgroup per (bucket b, group g) segment, on XCD b % 8 (workgroup i
@@ -1362,9 +1203,9 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             const size_t gb = (size_t)(p.tile / kRunGroup) * stg.nb;
             p.g0 = stg.gb[gb];
             if (tid < stg.nb) {
-                const size_t o = (size_t)tid * stg.ostride + p.tile;
+                const size_t o = (size_t)p.tile * stg.ostride + tid;  // the tile's run table: contiguous
                 p.st0 = stg.offt[o];
-                p.st1 = stg.offt[o + stg.ostride];
+                p.st1 = stg.offt[o + 1];
                 p.gbt = stg.gb[gb + tid];
                 p.off2 = stg.off2[o];
             }
@@ -1379,10 +1220,13 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     auto run_lookup = [&](uint32_t q, uint32_t pre) {  // index of element q's word, relative to g0
         const uint32_t k = (uint32_t)__shfl((int)pre, (int)(q >> 6), 64) +
                            (uint32_t)__popcll(s_sbm[q >> 6] & (~0ull >> (63 - (q & 63)))) - 1u;
-        return s_ksrc[k] + q;
+        return s_ksrc[k & (kStageMaxNB - 1)] + q;  // (an element outside every run is never loaded)
     };
     auto round2 = [&](const Pre& p, uint32_t b0, uint32_t pre) {  // words [b0, b0 + kU * 256) of the tile
-        const uint32_t ne = (uint32_t)((int64_t)p.an - (int64_t)p.a0);
+        const uint32_t ne_all = (uint32_t)((int64_t)p.an - (int64_t)p.a0);
+        // a tile past cap_a staged nothing (its run table is empty): no words to fetch — the run
+        // lookup of an element outside every run would index s_ksrc[-1]
+        const uint32_t ne = ne_all > (uint32_t)cap_a ? 0u : ne_all;
         if constexpr (STAGED) {
             const uint32_t* __restrict__ St = stg.s + p.g0;
             const uint32_t* __restrict__ Dt = stg.d + p.g0;
@@ -1843,9 +1687,9 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
         const size_t gb = (size_t)(tile / kRunGroup) * stg.nb;
         g0 = stg.gb[gb];
         if (tid < stg.nb) {
-            const size_t o = (size_t)tid * stg.ostride + tile;
+            const size_t o = (size_t)tile * stg.ostride + tid;
             m_st = stg.offt[o];
-            m_len = stg.offt[o + stg.ostride] - m_st;
+            m_len = stg.offt[o + 1] - m_st;
             m_src = (uint32_t)(stg.gb[gb + tid] - g0) + stg.off2[o];
         }
         if (tid < 64) s_sbm[tid] = 0ull;
@@ -2202,6 +2046,380 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     STAMP(6);
 }
 
+// ------------------------------------------------------------------------------------------
+// Split row-lane pipeline, the staged default: the main kernel's two halves as
+// two launches, so that the compute half runs without block barriers at full occupancy.
+//   lpr_unsort_kernel (M1)  staged descriptors back into entry order (DE, tile-strided)
+//   lpr_wave_kernel   (M2)  one wave per 64 rows, independent of every other wave
+// Measured reason: the persistent main kernel is latency-bound (64% of wave cycles
+// waiting at 4 waves per SIMD, six block barriers per tile) and insensitive to its fetch volume
+// (twice longer staged runs: -2%).
+
+// M1: one workgroup per super-tile (one 256-thread quarter per tile, kPartTiles tiles): the tile's
+// run table (OFFT / OFF2 / GB) -> element -> run lookup (start bitmap + popcount), the S/D words of
+// its runs (the super-tile's runs of a bucket are adjacent, so the four quarters' loads of a bucket
+// cover one contiguous range), each D word scattered by S's entry index into LDS, then the tile's
+// descriptors stored in entry order at DE[tile * cap_a + e], coalesced. A descriptor is the W32
+// word (n <= 2 entries inline; code 3 = more: count << 26 | feature). Heavy tiles (more than cap_a
+// entries) staged nothing and are skipped.
+template <typename IP>
+__global__ void __launch_bounds__(kPBlock)
+lpr_unsort_kernel(const IP* __restrict__ Ap, int64_t n_rows, LprStage stg, int cap_a, unsigned n_tiles, unsigned s8,
+                  uint32_t* __restrict__ DE) {
+    extern __shared__ __align__(16) uint32_t s_desc[];  // [kPartTiles][cap_a]
+    __shared__ uint32_t s_ksrc[kPartTiles][kStageMaxNB];
+    __shared__ uint64_t s_sbm[kPartTiles][64];
+    __shared__ uint32_t s_wnz[kPBlock / 64];
+    if (*stg.gate == 0) return;  // uniform (written only by earlier launches)
+    const int tid = threadIdx.x, q = tid >> 8, qt = tid & (kBlock - 1), w = tid >> 6, lane = tid & 63;
+    const unsigned t0 = xcd_tile(blockIdx.x, s8) * kPartTiles;
+    if (t0 >= n_tiles) return;  // uniform
+    const unsigned t = t0 + q;
+    int64_t ea = 0, ne = 0;
+    if (t < n_tiles) {
+        const int64_t row0 = (int64_t)t * kLprRows;
+        ea = (int64_t)Ap[row0];
+        ne = (int64_t)Ap[std::min<int64_t>(row0 + kLprRows, n_rows)] - ea;
+    }
+    const uint32_t n = ne <= cap_a ? (uint32_t)ne : 0u;  // quarter-uniform
+    uint32_t m_st = 0, m_len = 0, m_src = 0;
+    int64_t g0 = 0;
+    if (n > 0) {
+        const size_t gb = (size_t)(t / kRunGroup) * stg.nb;
+        g0 = stg.gb[gb];
+        if (qt < stg.nb) {
+            const size_t o = (size_t)t * stg.ostride + qt;
+            m_st = stg.offt[o];
+            m_len = stg.offt[o + 1] - m_st;
+            m_src = (uint32_t)(stg.gb[gb + qt] - g0) + stg.off2[o];
+        }
+    }
+    if (qt < 64) s_sbm[q][qt] = 0ull;
+    const uint64_t nzb = __ballot(m_len > 0);
+    if (lane == 0) s_wnz[w] = (uint32_t)__popcll(nzb);
+    __syncthreads();
+    // run k of the tile (k-th nonempty bucket) starts at element st: bit st of the start bitmap,
+    // its words at S/D index s_ksrc[k] + element (relative to the group's first segment)
+    if (m_len > 0) {
+        uint32_t k = (uint32_t)__popcll(nzb & ((1ull << lane) - 1ull));
+        for (int i = 4 * q; i < w; ++i) k += s_wnz[i];
+        s_ksrc[q][k] = m_src - m_st;
+        atomicOr(reinterpret_cast<unsigned long long*>(&s_sbm[q][m_st >> 6]), 1ull << (m_st & 63));
+    }
+    __syncthreads();
+    const uint32_t c = (uint32_t)__popcll(s_sbm[q][lane]);
+    const uint32_t pre = wave_scan_dpp(c) - c;  // set bits in the words below word `lane`
+    const uint32_t* __restrict__ St = stg.s + g0;
+    const uint32_t* __restrict__ Dt = stg.d + g0;
+    uint32_t* sd = s_desc + (size_t)q * cap_a;
+    constexpr int kU = 12;
+    // quarter-uniform trip count: every lane of a wave takes part in the shuffle
+    for (uint32_t b0 = 0; b0 < n; b0 += kU * kBlock) {
+        const uint32_t q0 = b0 + qt;
+        uint32_t sv[kU], dv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint32_t e = std::min(q0 + u * kBlock, n - 1);
+            const uint32_t k = (uint32_t)__shfl((int)pre, (int)(e >> 6), 64) +
+                               (uint32_t)__popcll(s_sbm[q][e >> 6] & (~0ull >> (63 - (e & 63)))) - 1u;
+            const uint32_t i = s_ksrc[q][k] + e;
+            sv[u] = q0 + u * kBlock < n ? __builtin_nontemporal_load(St + i) : 0u;
+            dv[u] = q0 + u * kBlock < n ? __builtin_nontemporal_load(Dt + i) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (q0 + u * kBlock < n) sd[sv[u] >> 20] = dv[u];
+    }
+    __syncthreads();
+    uint32_t* __restrict__ DEt = DE + (size_t)t * cap_a;
+    for (uint32_t e = qt; e < n; e += kBlock) DEt[e] = sd[e];
+}
+
+// t-th product's (sign << 14 | col) of an entry with DE descriptor d (code 3: W[feature])
+__device__ __forceinline__ uint32_t lpr_slot_de(uint32_t d, uint32_t t, const uint64_t* W, const uint16_t* O) {
+    if ((d >> 30) < 3) return (d >> (15 * t)) & 0x7fffu;
+    const uint64_t w = W[d & kW32J];
+    if ((w >> 61) != 7) return (uint32_t)(w >> (15 * t)) & 0x7fffu;
+    const uint32_t e = O[(w & kLow61) + 1 + t];
+    return ((e & 0x8000u) >> 1) | (e & 0x3fffu);
+}
+
+// M2: one 64-thread workgroup = one wave = one 64-row unit (tile rb / 4, wave rb % 4 of the
+// workspace layout the scan / copy / heavy kernels read). Round 1: the unit's row pointers (and
+// its tile's entry count: a heavy tile goes to the exact path whole). Round 2: descriptors and
+// values of up to kWaveSteps x 64 entries, coalesced, all in flight together. The flat pass then
+// runs from registers: per step, an entry's row from the row-start bitmap, its products' kept
+// prefix (DPP scan) = their place in the slot, in first-touch order. Side entries (> 2 R entries)
+// keep a gap, filled after the pass from their W words (gathered once the pass has listed them).
+// The row phase is lpr_main_kernel's: Bloom check, exact path for flagged rows, optional sort,
+// row metadata, the slot stored coalesced.
+constexpr int kWaveSteps = 12;                 // flat-pass steps per load round (avg KDD2012: 11)
+constexpr int kWaveMaxSteps = 32;              // entries per unit beyond 32 x 64 -> heavy tile
+constexpr int kWaveSide = 32;                  // side entries per unit beyond this -> heavy tile
+constexpr int kWaveScr = 128;                  // exact-path scratch (products of one row)
+__host__ __device__ inline size_t lpr_wave_lds_bytes(uint32_t slot, size_t vs) {
+    return ((2 * (size_t)slot + 15) & ~size_t(15)) + ((vs * (size_t)slot + 15) & ~size_t(15)) +
+           ((2 * (size_t)kWaveScr + 15) & ~size_t(15)) + vs * kWaveScr;
+}
+template <typename T, typename IP>
+__global__ void __launch_bounds__(64)
+lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const T* __restrict__ Ax,
+                const uint32_t* __restrict__ DE, const uint32_t* __restrict__ gate, int cap_a, unsigned n_tiles,
+                int order, LprSpace sp, Workspace* ws) {
+    extern __shared__ __align__(16) unsigned char lds[];  // slot columns, slot values, exact-path scratch
+    __shared__ uint64_t s_flag[kWaveMaxSteps];            // row-start bitmap over the unit's entries
+    __shared__ uint64_t s_susp;                           // rows flagged for the exact path
+    __shared__ uint16_t s_kst[64];
+    __shared__ uint8_t s_nz2row[64];
+    __shared__ uint16_t s_sfk[kWaveSide];                 // side entry's slot position (0xffff: zero x)
+    __shared__ T s_sfx[kWaveSide];                        // ... its value
+    __shared__ uint32_t s_sfj[kWaveSide];                 // ... its feature
+    if (*gate == 0) return;  // uniform: the device chose direct gathers for this call
+    const unsigned rb = blockIdx.x, tile = rb >> 2;  // unit rb = wave rb % 4 of tile rb / 4
+    const int lane = threadIdx.x;
+    const int64_t row0 = (int64_t)rb * 64;
+    if (tile >= n_tiles) return;
+    if (row0 >= n_rows) {  // the last tile's empty units
+        if (lane == 0) sp.cnt[rb] = 0u;
+        return;
+    }
+    const int nrows = (int)std::min<int64_t>(64, n_rows - row0);
+    const int64_t trow0 = (int64_t)tile * kLprRows;
+    const int64_t ta = (int64_t)Ap[trow0];
+    const int64_t tn = (int64_t)Ap[std::min<int64_t>(trow0 + kLprRows, n_rows)] - ta;
+    const uint32_t E0 = (uint32_t)((int64_t)Ap[row0] - ta), E1 = (uint32_t)((int64_t)Ap[row0 + nrows] - ta);
+    const uint32_t rs = lane < nrows ? (uint32_t)((int64_t)Ap[row0 + lane] - ta) : E1;
+    auto go_heavy = [&]() {  // the heavy path takes the whole tile (idempotent over its four units)
+        if (lane == 0 && atomicOr(&sp.tflag[tile], 1u) == 0u) sp.hlist[atomicAdd(&ws->n_deferred, 1u)] = tile;
+    };
+    const uint32_t nsteps = (E1 - E0 + 63) >> 6;
+    if (tn > cap_a || nsteps > (uint32_t)kWaveMaxSteps) {  // uniform: M1 staged nothing / too many
+        go_heavy();
+        return;
+    }
+    const uint32_t* __restrict__ DEt = DE + (size_t)tile * cap_a;
+    const T* __restrict__ Axt = Ax + ta;
+    uint32_t dv[kWaveSteps];
+    T xv[kWaveSteps];
+    auto load_round = [&](uint32_t j0) {
+#pragma unroll
+        for (int u = 0; u < kWaveSteps; ++u) {
+            const uint32_t e = E0 + 64 * (j0 + u) + lane;
+            const uint32_t ec = std::min(e, E1 > E0 ? E1 - 1 : E0);
+            const uint32_t d = DEt[ec];
+            const T x = Axt[ec];
+            dv[u] = e < E1 ? d : 0u;
+            xv[u] = e < E1 ? x : T(0);
+        }
+    };
+    if (nsteps > 0) load_round(0);  // (an empty unit loads nothing: E0 may be the array's end)
+    const uint32_t re = __shfl_down(rs, 1, 64);
+    const uint32_t rend = lane == nrows - 1 ? E1 : (lane < nrows ? re : E1);
+    const bool valid = lane < nrows;
+    const bool nonempty = valid && rend > rs;
+    uint16_t* cb = reinterpret_cast<uint16_t*>(lds);
+    T* vb = reinterpret_cast<T*>(lds + ((2 * (size_t)sp.slot + 15) & ~size_t(15)));
+    uint16_t* scol = reinterpret_cast<uint16_t*>(lds + ((2 * (size_t)sp.slot + 15) & ~size_t(15)) +
+                                                 ((sizeof(T) * (size_t)sp.slot + 15) & ~size_t(15)));
+    T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(scol) + ((2 * (size_t)kWaveScr + 15) & ~size_t(15)));
+    for (uint32_t k = lane; k < nsteps; k += 64) s_flag[k] = 0ull;
+    if (lane == 0) s_susp = 0ull;
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t ne_mask = __ballot(nonempty);
+    if (nonempty) {
+        const uint32_t b = rs - E0;
+        atomicOr(reinterpret_cast<unsigned long long*>(&s_flag[b >> 6]), 1ull << (b & 63));
+        s_nz2row[__builtin_popcountll(ne_mask & ((1ull << lane) - 1))] = (uint8_t)lane;
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t carry_r = 0, carry_k = 0, nside = 0;
+    bool bad = false;
+    const T nmag = -mag;
+    auto step = [&](uint32_t j, uint32_t d, T x) {
+        const uint32_t e = E0 + 64 * j + lane;
+        const bool ve = e < E1;
+        const uint64_t fw = s_flag[j];
+        const uint32_t nr = carry_r + (uint32_t)__builtin_popcountll(fw & ((2ull << lane) - 1)) - 1u;
+        const uint32_t row = s_nz2row[nr & 63];
+        const uint32_t n = d >> 30;
+        const uint32_t np = n < 3 ? n : (d >> 26) & 15u;  // code 3: a side entry (count in the word)
+        const bool nzx = tmul<T>(x, mag) != T(0);         // all products of an entry share |x * mag|
+        const uint32_t kc = nzx ? np : 0u;
+        const uint32_t kinc = wave_scan_dpp(kc);
+        const uint32_t K = carry_k + kinc - kc;
+        if (ve && ((fw >> lane) & 1ull)) s_kst[row] = (uint16_t)K;  // the row's first entry
+        const uint32_t sl0 = d & 0x7fffu, sl1 = (d >> 15) & 0x7fffu;
+        if (n < 3 && kc >= 1 && K < sp.slot) {
+            cb[K] = (uint16_t)(sl0 & 0x3fffu);
+            vb[K] = tadd<T>(T(0), tmul<T>(x, (sl0 & 0x4000u) ? nmag : mag));
+        }
+        if (n < 3 && kc >= 2 && K + 1 < sp.slot) {
+            cb[K + 1] = (uint16_t)(sl1 & 0x3fffu);
+            vb[K + 1] = tadd<T>(T(0), tmul<T>(x, (sl1 & 0x4000u) ? nmag : mag));
+        }
+        // side entries keep a gap [K, K + np) in the slot, filled after the pass; a zero product
+        // is not in the slot: its row takes the exact path
+        const bool side = ve && n == 3;
+        const uint64_t sm = __ballot(side);
+        if (side) {
+            const uint32_t k = nside + (uint32_t)__builtin_popcountll(sm & ((1ull << lane) - 1));
+            if (k < (uint32_t)kWaveSide) {
+                s_sfk[k] = kc ? (uint16_t)K : (uint16_t)0xffffu;
+                s_sfx[k] = x;
+                s_sfj[k] = d & kW32J;
+            }
+            if (np == 15) bad = true;  // 15 or more entries: the count is not exact -> heavy tile
+        }
+        nside += (uint32_t)__builtin_popcountll(sm);
+        if (ve && np > 0 && !nzx) atomicOr(reinterpret_cast<unsigned long long*>(&s_susp), 1ull << row);
+        carry_k += __builtin_amdgcn_readlane(kinc, 63);
+        carry_r += (uint32_t)__builtin_popcountll(fw);
+    };
+    for (uint32_t j0 = 0; j0 < nsteps; j0 += kWaveSteps) {
+        if (j0 > 0) load_round(j0);  // rare: more than kWaveSteps x 64 entries
+#pragma unroll
+        for (int u = 0; u < kWaveSteps; ++u)
+            if (j0 + u < nsteps) step(j0 + u, dv[u], xv[u]);
+    }
+    bad = __ballot(bad) != 0 || nside > (uint32_t)kWaveSide;
+    bool overflow = carry_k > sp.slot;
+    // side fill: every side entry's products into its gap, in R's storage order
+    if (!bad && (uint32_t)lane < nside) {
+        const uint64_t sw = R.W[s_sfj[lane]];
+        const uint32_t k0 = s_sfk[lane];
+        if (k0 != 0xffffu) {
+            const T x = s_sfx[lane];
+            const bool rec = (sw >> 61) == 7;
+            const uint32_t np = rec ? R.O[sw & kLow61] : (uint32_t)(sw >> 61);
+            for (uint32_t t = 0; t < np && k0 + t < sp.slot; ++t) {
+                uint32_t sl;
+                if (rec) {
+                    const uint32_t e = R.O[(sw & kLow61) + 1 + t];
+                    sl = ((e & 0x8000u) >> 1) | (e & 0x3fffu);
+                } else {
+                    sl = (uint32_t)(sw >> (15 * t)) & 0x7fffu;
+                }
+                cb[k0 + t] = (uint16_t)(sl & 0x3fffu);
+                vb[k0 + t] = tadd<T>(T(0), tmul<T>(x, (sl & 0x4000u) ? -mag : mag));
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (bad) {  // uniform
+        go_heavy();
+        return;
+    }
+    // ---- per row: kept count and a Bloom check of its columns (3 x 64-bit filters in registers)
+    const uint32_t kst = nonempty ? s_kst[lane] : 0u;
+    const uint64_t after = ne_mask & ~((2ull << lane) - 1);  // the next non-empty row ends this one
+    const int nx = after ? __builtin_ctzll(after) : 64;
+    const uint32_t kst_next = __shfl(kst, nx & 63, 64);
+    const uint32_t kend_r = nx < 64 ? kst_next : carry_k;
+    uint32_t kept = nonempty ? kend_r - kst : 0u;
+    bool hit = false;
+    if (!overflow) {
+        uint64_t b0 = 0, b1 = 0, b2 = 0;
+        for (uint32_t q = kst; q < kend_r; ++q) {
+            const uint32_t col = cb[q];
+            const uint64_t m0 = 1ull << (col & 63), m1 = 1ull << ((col >> 6) & 63), m2 = 1ull << lpr_h2(col);
+            hit |= (b0 & m0) && (b1 & m1) && (b2 & m2);
+            b0 |= m0;
+            b1 |= m1;
+            b2 |= m2;
+        }
+    }
+    uint64_t todo = s_susp | __ballot(hit);  // lane == row within the unit
+    if (__ballot(overflow)) todo = 0;
+    // exact path, one flagged row at a time, the whole wave on it: its products in sequence order
+    // into the scratch, then every product checks for an earlier one of its column (first touch);
+    // a leader sums its group in order; kept leaders land in the row's slot range in that order
+    while (todo) {
+        const int R0 = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        const uint32_t a0 = __shfl(rs, R0, 64), a1 = __shfl(rend, R0, 64), kR = __shfl(kst, R0, 64);
+        uint32_t nprod = 0;
+        for (uint32_t e0 = a0; e0 < a1; e0 += 64) {
+            const uint32_t e = e0 + lane;
+            const bool in = e < a1;
+            const uint32_t d = in ? DEt[e] : 0u;
+            const T x = in ? Axt[e] : T(0);
+            const uint32_t np = in ? ((d >> 30) < 3 ? (d >> 30) : (d >> 26) & 15u) : 0u;
+            const uint32_t inc = wave_scan_dpp(np);
+            const uint32_t q0 = nprod + inc - np;
+            for (uint32_t t = 0; t < np; ++t)
+                if (q0 + t < (uint32_t)kWaveScr) {
+                    const uint32_t sl = lpr_slot_de(d, t, R.W, R.O);
+                    scol[q0 + t] = (uint16_t)(sl & 0x3fffu);
+                    sval[q0 + t] = tmul<T>(x, (sl & 0x4000u) ? -mag : mag);
+                }
+            nprod += __builtin_amdgcn_readlane(inc, 63);
+        }
+        if (nprod > (uint32_t)kWaveScr) {
+            overflow = true;
+            break;
+        }
+        __builtin_amdgcn_wave_barrier();
+        uint32_t nk = 0;
+        for (uint32_t q0 = 0; q0 < nprod; q0 += 64) {
+            const uint32_t q = q0 + lane;
+            bool lead = q < nprod;
+            T sum = T(0);
+            if (lead) {
+                const uint16_t cq = scol[q];
+                for (uint32_t b = 0; b < q && lead; ++b) lead = scol[b] != cq;
+                if (lead) {
+                    sum = tadd<T>(T(0), sval[q]);
+                    for (uint32_t b = q + 1; b < nprod; ++b)
+                        if (scol[b] == cq) sum = tadd<T>(sum, sval[b]);
+                }
+            }
+            const bool keep = lead && sum != T(0);
+            const uint32_t ki = wave_scan_dpp(keep ? 1u : 0u);
+            if (keep) {
+                if (kR + nk + ki - 1 >= sp.slot) overflow = true;
+                else {
+                    cb[kR + nk + ki - 1] = scol[q];
+                    vb[kR + nk + ki - 1] = sum;
+                }
+            }
+            nk += __builtin_amdgcn_readlane(ki, 63);
+        }
+        if (lane == R0) kept = nk;
+        __builtin_amdgcn_wave_barrier();
+    }
+    // a row that gained entries in the exact path (side products not in the slot) must still end
+    // before the next row's range
+    if (kst + kept > kend_r && nonempty) overflow = true;
+    if (__ballot(overflow)) {  // this unit cannot finish on the fast path: the whole tile goes heavy
+        go_heavy();
+        return;
+    }
+    if (order == RP_ORDER_SORTED && kept > 1) {  // ascending columns inside the row's slot range
+        for (uint32_t a = kst + 1; a < kst + kept; ++a) {
+            const uint16_t kc = cb[a];
+            const T kv = vb[a];
+            uint32_t b = a;
+            while (b > kst && cb[b - 1] > kc) {
+                cb[b] = cb[b - 1];
+                vb[b] = vb[b - 1];
+                --b;
+            }
+            cb[b] = kc;
+            vb[b] = kv;
+        }
+    }
+    if (valid) sp.rowmeta[(size_t)row0 + lane] = (kst << 16) | kept;
+    const uint32_t wtot = __builtin_amdgcn_readlane(wave_scan_dpp(valid ? kept : 0u), 63);
+    if (lane == 0) sp.cnt[rb] = wtot;
+    __builtin_amdgcn_wave_barrier();
+    uint16_t* __restrict__ oc = sp.cols + (size_t)rb * sp.slot;
+    T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + (size_t)rb * sp.slot;
+    for (uint32_t q = lane; q < carry_k; q += 64) {
+        oc[q] = cb[q];
+        ov[q] = vb[q];
+    }
+}
+
 // heavy tiles, pass 0: the exact dense accumulator counts their rows (grid-stride over the list);
 // the count goes to the tile's first wave slot, the other three are zeroed
 template <typename T, typename IP>
@@ -2504,6 +2722,7 @@ struct rp_projector {
     int opt_defer_ticks = -1;   // -1 default
     int64_t opt_chunk_rows = 0; // 0 default
     int opt_host_threads = -1;  // -1 default
+    int opt_lpr_split = -1;     // -1 default (split), 0 the persistent main kernel, 1 split
     // generic
     DevBuf Bp, Bj, Bx32, Bx64;
     // internal workspace and host-path staging
@@ -2545,9 +2764,10 @@ size_t lds_bytes_for(const Caps& c, int value_size, int64_t p) {
     return std::max(L.total, heavy_lds_bytes(p, (size_t)value_size));
 }
 
-// Staged-gather plan and workspace carve-up (offsets in bytes from the workspace start):
-//   [Workspace header + look-back states] [TE i64 x tiles] [OFFT u16 x (nb+1) x ostride]
-//   [S u32 x nnz] [D u32 x nnz] [SX value x nnz]   (value size vs: 8 when only sizing)
+// Launch plan and workspace carve-up (offsets in bytes from the workspace start). Tile pipeline:
+//   [Workspace header + look-back states] [deferred list, pool offsets, headers, pool]. Row-lane:
+//   [header + scan states + heavy flags] [carry slots + gate] [wave counts, offsets, heavy list,
+//   row metadata, slots] [staged: OFFT, OFF2, GB, FILL, S, D, DE]   (value size vs: 8 when sizing)
 struct Plan {
     Caps caps;
     int64_t n_tiles = 0;
@@ -2555,8 +2775,7 @@ struct Plan {
     bool defer = false;
     int sb = 0, nb = 0;
     uint32_t ostride = 0;
-    size_t head = 0, dlist = 0, pofs = 0, dhdr = 0, pcols = 0, pvals = 0, te = 0, offt = 0, s = 0,
-           d = 0, sx = 0;
+    size_t head = 0, dlist = 0, pofs = 0, dhdr = 0, pcols = 0, pvals = 0, offt = 0, s = 0, d = 0;
     unsigned long long pool_cap = 0;
     size_t total = 0;
     // row-lane pipeline (lpr_*): tiles of kLprRows rows, every tile's output in a fixed slot
@@ -2572,13 +2791,14 @@ struct Plan {
     size_t off2 = 0, gb = 0, fill = 0;  // staged runs (lpr_reserve_kernel, lpr_partition_kernel)
     int64_t sd_words = 0;               // S / D capacity (words)
     unsigned groups = 0;
+    bool split = false;                 // staged: unsort (M1) + wave kernel (M2) instead of lpr_main_kernel
+    size_t de = 0;                      // M1 -> M2 descriptors, n_tiles x cap_a words
 };
 
 constexpr unsigned kDeferCopyGrid = 32768;  // copy workgroups (grid-stride over the deferred list)
 constexpr int kDeferPolls = 4;                 // polls before a 256-row tile defers (time budget off)
 constexpr int kDeferPollsShort = 8;            // ... and before a tile of fewer than 128 rows does
 constexpr int kDeferTicks = 800;               // 256-row tiles: wait budget, 8 us (defer_ticks_setting)
-constexpr bool kStageAuto = false;              // auto picks staging (off until it measures faster)
 constexpr int64_t kStageMinNnz = 1 << 22;      // auto: stage only launches this large
 // rp_project_stream's default chunk: configs[1] host CSR in/out measured 475 M rows/s with 4M-row
 // chunks, 544 M with 2M (shorter fill and drain of the upload/compute/download pipeline)
@@ -2654,11 +2874,14 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
                 pl.gated = h->stage_mode == -1;
                 pl.sb = sb;
                 pl.nb = std::max(nbk(sb), 1);
-                pl.ostride = (uint32_t)((pl.n_tiles + 31) & ~int64_t(31));
+                // run tables tile-major: a tile's (nb + 1) bucket starts and nb run positions are
+                // contiguous (one or two lines per tile for the partition's stores and the main
+                // kernel's loads, instead of one line per bucket)
+                pl.ostride = (uint32_t)((pl.nb + 1 + 7) & ~7);
                 pl.groups = (unsigned)((pl.n_tiles + kRunGroup - 1) / kRunGroup);
                 pl.offt = pl.total;
-                pl.off2 = pl.offt + al(2 * (size_t)(pl.nb + 1) * pl.ostride);
-                pl.gb = pl.off2 + al(4 * (size_t)pl.nb * pl.ostride);
+                pl.off2 = pl.offt + al(2 * (size_t)pl.ostride * (size_t)pl.n_tiles);
+                pl.gb = pl.off2 + al(4 * (size_t)pl.ostride * (size_t)pl.n_tiles);
                 const size_t nseg = (size_t)pl.groups * pl.nb;
                 pl.fill = pl.gb + al(8 * (nseg + 1));
                 // staged entries of one chunk: all of them, or (several chunks) at most cap_a per
@@ -2670,6 +2893,11 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
                 pl.s = pl.fill + al(4 * nseg);
                 pl.d = pl.s + al(4 * sd);
                 pl.total = pl.d + al(4 * sd);
+                pl.split = h->opt_lpr_split != 0;
+                if (pl.split) {
+                    pl.de = pl.total;
+                    pl.total = pl.de + al(4 * (size_t)pl.n_tiles * (size_t)pl.caps.cap_a);
+                }
             }
         }
         return pl;
@@ -2690,26 +2918,7 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
         pl.pvals = pl.pcols + al(2 * (size_t)pl.pool_cap);
         pl.total = pl.pvals + al((size_t)vs * (size_t)pl.pool_cap);
     }
-    const bool can = h->layout == RP_LAYOUT_PACKED && h->W32.p && nnz_a > 0 && pl.n_tiles > 0;
-    const bool want = h->stage_mode == 1 ||
-                      (h->stage_mode == -1 && kStageAuto && nnz_a >= kStageMinNnz &&
-                       8 * h->m >= kStageMinTable);
-    if (!(can && want && allow_stage)) return pl;
-    int sb = h->stage_sb > 0 ? h->stage_sb : 19;  // 2 MB W32 slice: stays in an XCD's 4 MB L2
-    auto nbk = [&](int b) { return (int)((h->m + ((int64_t)1 << b) - 1) >> b); };
-    while (h->stage_sb <= 0 && nbk(sb) > kStageMaxNB && sb < 20) ++sb;
-    if (sb < 1 || sb > 20 || nbk(sb) > kStageMaxNB) return pl;
-    pl.staged = true;
-    pl.sb = sb;
-    pl.nb = std::max(nbk(sb), 1);
-    pl.ostride = (uint32_t)((pl.n_tiles + 31) & ~int64_t(31));
-    pl.te = pl.total;
-    pl.offt = pl.te + al(8 * (size_t)pl.n_tiles);
-    pl.s = pl.offt + al(2 * (size_t)(pl.nb + 1) * pl.ostride);
-    pl.d = pl.s + al(4 * (size_t)nnz_a);
-    pl.sx = pl.d + al(4 * (size_t)nnz_a);
-    pl.total = pl.sx + al((size_t)vs * (size_t)nnz_a);
-    return pl;
+    return pl;  // the tile pipeline gathers R's descriptors directly (its staged gather was removed)
 }
 
 // Polls before a tile defers. Measured optimum differs with the tile shape and the gather pattern
@@ -2735,28 +2944,27 @@ int defer_polls_setting(const rp_projector* h, const Caps& caps) {
     return caps.rpt >= 128 ? kDeferPolls : kDeferPollsShort;
 }
 
-template <typename T, typename IP, typename OP, typename OI, typename RL, bool STAGED, int WPE = 1>
+template <typename T, typename IP, typename OP, typename OI, typename RL, int WPE = 1>
 int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
                 int order, Workspace* ws, unsigned n_tiles, const Plan& pl, size_t lds,
-                hipStream_t st, const uint32_t* S, const T* SX, const uint32_t* D) {
-    if constexpr (WPE == 1 && !STAGED && std::is_same<T, float>::value && std::is_same<RL, PackedR>::value) {
+                hipStream_t st) {
+    if constexpr (WPE == 1 && std::is_same<T, float>::value && std::is_same<RL, PackedR>::value) {
         // 7 tiles per CU fit the LDS (static arrays ~1.6 KB per tile): take the 7-wave build
         if (lds + 2048 <= 160 * 1024 / 7)
-            return launch_main<T, IP, OP, OI, RL, STAGED, 7>(R, mag, h, a, c, order, ws, n_tiles, pl, lds,
-                                                             st, S, SX, D);
+            return launch_main<T, IP, OP, OI, RL, 7>(R, mag, h, a, c, order, ws, n_tiles, pl, lds, st);
     }
-    HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED, WPE>,
+    HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, WPE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     char* base = reinterpret_cast<char*>(ws);
     DeferSpace dfr{reinterpret_cast<unsigned int*>(base + pl.dlist),
                    reinterpret_cast<unsigned long long*>(base + pl.pofs),
                    reinterpret_cast<uint16_t*>(base + pl.dhdr), reinterpret_cast<uint16_t*>(base + pl.pcols),
                    reinterpret_cast<unsigned char*>(base + pl.pvals), pl.pool_cap};
-    hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL, STAGED, WPE>), dim3(n_tiles), dim3(kBlock), lds, st,
+    hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL, WPE>), dim3(n_tiles), dim3(kBlock), lds, st,
                        R, mag, (int)h->p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
                        (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order,
-                       ws, n_tiles, S, SX, D, dfr, pl.defer ? defer_polls_setting(h, pl.caps) : -1,
+                       ws, n_tiles, dfr, pl.defer ? defer_polls_setting(h, pl.caps) : -1,
                        pl.defer ? defer_ticks_setting(h, pl.caps) : 0);
     HIP_TRY(hipGetLastError());
     if (pl.defer) {
@@ -2805,11 +3013,12 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
         hipLaunchKernelGGL((lpr_reserve_kernel<IP>), dim3(1), dim3(kResBlock), 0, st, Ap, a->n_rows, (int)kLprRows,
                            (int64_t)h->m, pl.groups, pl.sb, pl.nb, pl.caps.cap_a, pl.sd_words, GB, FILL, gate);
         HIP_TRY(hipGetLastError());
-        const size_t plds = 4 * (size_t)pl.caps.cap_a;
+        const size_t plds = 4 * (size_t)kPartTiles * (size_t)pl.caps.cap_a;
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_partition_kernel<IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)plds));
-        hipLaunchKernelGGL((lpr_partition_kernel<IP>), dim3(8 * t8), dim3(kBlock), plds, st, Ap, a->indices,
-                           a->n_rows, pl.caps, n_tiles, t8, pl.sb, pl.nb, pl.ostride, OFFT, OFF2,
+        const unsigned n_st = (n_tiles + kPartTiles - 1) / kPartTiles, s8 = (n_st + 7) / 8;
+        hipLaunchKernelGGL((lpr_partition_kernel<IP>), dim3(8 * s8), dim3(kPBlock), plds, st, Ap, a->indices,
+                           a->n_rows, pl.caps, n_tiles, s8, pl.sb, pl.nb, pl.ostride, OFFT, OFF2,
                            (const int64_t*)GB, FILL, Sw, gate);
         HIP_TRY(hipGetLastError());
         const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * pl.groups;
@@ -2833,7 +3042,21 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
         const unsigned want = ((unsigned)(per_cu * cus) + 7u) & ~7u;
         return std::min(want, 8u * t8);
     };
-    if (pl.staged) {
+    if (pl.staged && pl.split) {
+        uint32_t* DE = reinterpret_cast<uint32_t*>(base + pl.de);
+        const size_t ulds = 4 * (size_t)kPartTiles * (size_t)pl.caps.cap_a;
+        HIP_TRY(hipFuncSetAttribute((const void*)lpr_unsort_kernel<IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)ulds));
+        const unsigned n_st = (n_tiles + kPartTiles - 1) / kPartTiles, s8 = (n_st + 7) / 8;
+        hipLaunchKernelGGL((lpr_unsort_kernel<IP>), dim3(8 * s8), dim3(kPBlock), ulds, st, Ap, a->n_rows, stg,
+                           pl.caps.cap_a, n_tiles, s8, DE);
+        HIP_TRY(hipGetLastError());
+        const size_t wlds = lpr_wave_lds_bytes(pl.lpr_slot, sizeof(T));
+        HIP_TRY(hipFuncSetAttribute((const void*)lpr_wave_kernel<T, IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)wlds));
+        hipLaunchKernelGGL((lpr_wave_kernel<T, IP>), dim3(4 * n_tiles), dim3(64), wlds, st, R, mag, a->n_rows, Ap, Ax,
+                           (const uint32_t*)DE, (const uint32_t*)gate, pl.caps.cap_a, n_tiles, order, sp, ws);
+    } else if (pl.staged) {
         const void* fn = (const void*)lpr_main_kernel<T, IP, true>;
         HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         hipLaunchKernelGGL((lpr_main_kernel<T, IP, true>), dim3(grid_for(fn)), dim3(kLprRows), lds, st, R, mag,
@@ -2908,33 +3131,8 @@ int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const 
                  hipStream_t st) {
     if constexpr (std::is_same<RL, PackedR>::value) {
         if (pl.lpr) return launch_lpr<T, IP, OP, OI>(R, mag, h, a, c, order, ws, pl, st);
-        if (pl.staged) {
-            char* base = reinterpret_cast<char*>(ws);
-            int64_t* TE = reinterpret_cast<int64_t*>(base + pl.te);
-            uint16_t* OFFT = reinterpret_cast<uint16_t*>(base + pl.offt);
-            uint32_t* S = reinterpret_cast<uint32_t*>(base + pl.s);
-            uint32_t* D = reinterpret_cast<uint32_t*>(base + pl.d);
-            T* SX = reinterpret_cast<T*>(base + pl.sx);
-            const size_t plds = (4 + sizeof(T)) * (size_t)pl.caps.cap_a;
-            HIP_TRY(hipFuncSetAttribute((const void*)stage_partition_kernel<T, IP>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds));
-            hipLaunchKernelGGL((stage_partition_kernel<T, IP>), dim3(n_tiles),
-                               dim3(kBlock), plds, st, (const IP*)a->indptr, a->indices,
-                               (const T*)a->data, a->n_rows, pl.caps, n_tiles, pl.sb, pl.nb,
-                               pl.ostride, S, SX, OFFT, TE);
-            HIP_TRY(hipGetLastError());
-            const unsigned groups = (n_tiles + kStageTB - 1) / kStageTB;
-            const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * groups;
-            hipLaunchKernelGGL(stage_gather_kernel, dim3(grid), dim3(kBlock), kStageMap, st,
-                               (const uint32_t*)h->W32.p, (const int64_t*)TE, n_tiles, pl.sb, pl.nb,
-                               pl.ostride, groups, (const uint16_t*)OFFT, (const uint32_t*)S, D);
-            HIP_TRY(hipGetLastError());
-            return launch_main<T, IP, OP, OI, RL, true>(R, mag, h, a, c, order, ws, n_tiles, pl,
-                                                        lds, st, S, SX, D);
-        }
     }
-    return launch_main<T, IP, OP, OI, RL, false>(R, mag, h, a, c, order, ws, n_tiles, pl, lds,
-                                                 st, nullptr, nullptr, nullptr);
+    return launch_main<T, IP, OP, OI, RL>(R, mag, h, a, c, order, ws, n_tiles, pl, lds, st);
 }
 
 template <typename T, typename RL>
@@ -3471,6 +3669,9 @@ int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value) {
         case RP_OPT_HOST_THREADS:
             h->opt_host_threads = (int)std::max<int64_t>(std::min<int64_t>(value, 256), -1);
             return RP_OK;
+        case RP_OPT_LPR_SPLIT:
+            h->opt_lpr_split = (int)std::max<int64_t>(std::min<int64_t>(value, 1), -1);
+            return RP_OK;
         default:
             return fail(RP_ERR_INVALID, "unknown option %d", option);
     }
@@ -3484,6 +3685,7 @@ int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* valu
         case RP_OPT_DEFER_TICKS: *value = h->opt_defer_ticks; return RP_OK;
         case RP_OPT_CHUNK_ROWS: *value = h->opt_chunk_rows; return RP_OK;
         case RP_OPT_HOST_THREADS: *value = h->opt_host_threads; return RP_OK;
+        case RP_OPT_LPR_SPLIT: *value = h->opt_lpr_split; return RP_OK;
         default: return fail(RP_ERR_INVALID, "unknown option %d", option);
     }
 }

@@ -26,7 +26,8 @@ from __future__ import annotations
 
 import numpy as np
 
-from .linalg import Vectors, make_vector
+from .linalg import SparseVector, Vectors, make_vector
+from .linalg import HAVE_PYSPARK as _HAVE_PYSPARK
 from .projector import get_projector
 
 __all__ = ["random_project_mappartitions_function", "random_project_map_function", "assemble_rows"]
@@ -97,10 +98,23 @@ def random_project_mappartitions_function(rdd_row_iterator, local_csr_matrix):
     cx = Cx.astype(np.float64)
 
     def vectors():
+        # one vector per row, built lazily as the caller iterates (the reference's zip is lazy too);
+        # the constructor is inlined: this loop is most of the partition's host time
+        # (boundary 0)
         bounds = Cp.tolist()  # Python ints: cheap per-row slicing
         s = bounds[0]
+        if _HAVE_PYSPARK:  # pragma: no cover
+            for e in bounds[1:]:
+                yield make_vector(p, cj[s:e], cx[s:e])
+                s = e
+            return
+        new, SV = object.__new__, SparseVector
         for e in bounds[1:]:
-            yield make_vector(p, cj[s:e], cx[s:e])
+            v = new(SV)
+            v.size = p
+            v.indices = cj[s:e]
+            v.values = cx[s:e]
+            yield v
             s = e
 
     if has_label:

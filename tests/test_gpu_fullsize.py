@@ -49,8 +49,19 @@ def project(P, Ap, Aj, Ax, order="scipy", slack=1.02):
     dev = Aj.device
     n = Ap.numel() - 1
     nnz_a = int(Aj.numel())
-    ws = torch.empty(P.workspace_bytes(n, nnz_a, dtype=Ax.dtype), dtype=torch.uint8, device=dev)
+    ws_bytes = P.workspace_bytes(n, nnz_a, dtype=Ax.dtype)
     cap = int(slack * nnz_a * P.nnz / P.m) + 65536
+    # the HBM budget, stated before anything is allocated: workspace + C (indptr, indices, values)
+    # must fit next to A in what the device has free; a shortfall is named, not an opaque OOM
+    c_bytes = (n + 1) * (8 if cap >= 2**31 else 4) + cap * (4 + Ax.element_size())
+    free, total = torch.cuda.mem_get_info(dev)
+    need = ws_bytes + c_bytes
+    assert need <= free - (1 << 30), (
+        f"HBM budget: workspace {ws_bytes / 2**30:.1f} GiB + C {c_bytes / 2**30:.1f} GiB = {need / 2**30:.1f} GiB "
+        f"> {free / 2**30:.1f} GiB free of {total / 2**30:.1f} GiB (A holds {torch.cuda.memory_allocated(dev) / 2**30:.1f} "
+        "GiB); 1 GiB kept for the allocator")
+    print(f"HBM budget: workspace {ws_bytes / 2**30:.1f} + C {c_bytes / 2**30:.1f} of {free / 2**30:.1f} GiB free")
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     for _ in range(2):
         Cp = torch.empty(n + 1, dtype=torch.int64 if cap >= 2**31 else torch.int32, device=dev)
         Cj = torch.empty(cap, dtype=torch.int32, device=dev)

@@ -1,6 +1,9 @@
-"""Staged gather: bucketed descriptor fetch + coalesced main kernel. Results must be
-bit-identical to the direct-gather kernel and to the oracle (CPU restatement of scipy csr_matmat)
-for every bucket width, order, dtype, tile shape and workspace arrangement."""
+"""Staged gather: bucketed descriptor fetch for the row-lane pipeline (super-tile
+partition, filtered gather, unsort + wave kernels or the persistent main kernel), and the tile
+pipeline under the same staging requests (it gathers directly since round 4: a staging request is
+accepted and ignored there). Results must be bit-identical to the direct-gather kernels and to the
+oracle (CPU restatement of scipy csr_matmat) for every bucket width, order, dtype, tile shape and
+workspace arrangement."""
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -36,7 +39,7 @@ def test_staged_kdd_vs_oracle(R2m, shift, powerlaw):
     rng = np.random.default_rng(100 + shift + powerlaw)
     A = kdd_like(rng, 60_000, R2m.shape[0], powerlaw=powerlaw, values="normal")
     P = _staged(R2m, shift)
-    assert P.workspace_bytes(A.shape[0], A.nnz) >= 8 * A.nnz  # S + D staging buffers
+    assert P.plan(A.shape[0], A.nnz) == {"pipeline": "tile", "staged": False, "bucket_shift": 0}
     want = oracle_product(A, R2m)
     assert_same_csr(P.matmul(A), *want)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
@@ -64,7 +67,8 @@ def test_staged_f64_and_heavy_tiles():
 
 
 def test_staged_equals_direct_cfg4_shape():
-    """100 nnz/row power-law rows over p=1024 (config 4 shape, m scaled to 2M)."""
+    """100 nnz/row power-law rows over p=1024 (config 4 shape, m scaled to 2M): the tile pipeline with
+    and without a staging request gives the same bits."""
     rng = np.random.default_rng(4)
     m, p = 2_000_000, 1024
     R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
@@ -271,16 +275,18 @@ def _rows(rng, k, pool, m, dtype=np.float32):
                           np.concatenate([[0], np.cumsum(k)])), shape=(n, m))
 
 
-def _check_rowlane_staged(R, A, shift, staged=True):
+def _check_rowlane_staged(R, A, shift, staged=True, split=None):
     """Row-lane pipeline with staging forced on: host path in both orders against the oracle, then
     the device path, whose workspace records whether the staged gather ran (`staged`) or a segment
-    past its reserve sent the call to the direct kernel."""
+    past its reserve sent the call to the direct kernel. ``split``: 1 unsort + wave kernels (the
+    default), 0 the persistent main kernel."""
     import torch
 
     want = oracle_product(A, R)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     P = Projector(R)
     P.set_option("pipeline", "rowlane")
+    P.set_option("lpr_split", split)
     P.set_staging("on", shift)
     assert P.plan(A.shape[0], A.nnz) == {"pipeline": "rowlane", "staged": True, "bucket_shift": shift}
     assert_same_csr(P.matmul(A), *want)
@@ -314,6 +320,30 @@ def test_rowlane_staged_tile_of_3200_live_entries(R2m_p1k):
     A = sp.vstack([kdd_like(rng, 9 * 256, m, mean=11.2, values="normal"), _rows(rng, k, live, m),
                    kdd_like(rng, 9 * 256 + 31, m, mean=11.2, values="normal")]).tocsr()
     _check_rowlane_staged(R, A, 16)
+
+
+@pytest.mark.parametrize("split", [0, 1])
+def test_rowlane_staged_split_edges(R2m_p1k, split):
+    """The split staged pipeline (lpr_unsort_kernel + lpr_wave_kernel) and the persistent main kernel
+    on the same edge cases: a 64-row unit of 2240 entries (past the wave kernel's 32 x 64 entries:
+    the tile goes to the exact heavy path) next to light units of its tile, a unit whose 64 rows each
+    hold one feature with more than 2 R entries plus ordinary ones (more side entries than the
+    wave's side list: heavy), units of 13 steps (a second load round), empty rows, both orders."""
+    rng = np.random.default_rng(4 + split)
+    R = R2m_p1k
+    m = R.shape[0]
+    rl = np.diff(R.indptr)
+    side, live = np.flatnonzero(rl >= 3), np.flatnonzero(rl > 0)
+    big = sp.vstack([_rows(rng, np.full(64, 35), np.arange(m), m), _rows(rng, np.full(192, 3), np.arange(m), m)])
+    top = (_rows(rng, np.ones(64, int), side, m) + _rows(rng, np.full(64, 4), live, m)).tocsr()
+    top.sort_indices()
+    sidey = sp.vstack([top, _rows(rng, np.full(192, 9), np.arange(m), m)])
+    A = sp.vstack([kdd_like(rng, 5 * 256, m, values="normal"), big, _rows(rng, np.full(256, 13), np.arange(m), m),
+                   sp.csr_matrix((70, m), dtype=np.float32), sidey.astype(np.float32),
+                   kdd_like(rng, 7 * 256 + 9, m, values="normal")]).tocsr()
+    _check_rowlane_staged(R, A, 16, split=split)
+    _check_rowlane_staged(R, sp.vstack([kdd_like(rng, 9 * 256 + 5, m, mean=11.2, values="normal")]).tocsr(), 19,
+                          split=split)
 
 
 def test_rowlane_staged_dead_tiles_and_empty_rows(R2m_p1k):
