@@ -145,6 +145,8 @@ def main():
     ap.add_argument("--stage-shift", type=int, default=0, help="2^shift features per staging bucket (0 = auto)")
     ap.add_argument("--pipeline", choices=["auto", "tile", "rowlane"], default="auto",
                     help="force a kernel pipeline where it can run (results identical; measurements)")
+    ap.add_argument("--lpr-split", type=int, choices=[-1, 0, 1], default=-1,
+                    help="staged row-lane: 1 unsort + wave kernels (default), 0 the persistent main kernel")
     ap.add_argument("--cpu-sample-rows", type=int, default=None)
     ap.add_argument("--cpu-part-rows", type=int, default=100_000,
                     help="rows per recipe partition (one per core) in the CPU baseline")
@@ -205,7 +207,10 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    # RP_BENCH_FORCE_PG=1 at one rank: the process group, the RCCL broadcast of R's device image and
+    # the projector built from the received image all run (evidence for the N > 1 path on a 1-GPU box)
+    pg = world > 1 or os.environ.get("RP_BENCH_FORCE_PG") == "1"
+    if pg:
         if rehearse:
             dist.init_process_group("gloo")
         else:
@@ -226,7 +231,7 @@ def main():
         meta = None
     t_r = time.perf_counter() - t0
     t_bcast = 0.0
-    if world > 1:
+    if pg:
         box = [meta]
         dist.broadcast_object_list(box, src=0)
         meta = box[0]
@@ -239,7 +244,7 @@ def main():
             dist.broadcast(b, src=0)          # the recipe's sc.broadcast(R), once, over xGMI
         torch.cuda.synchronize()
         t_bcast = time.perf_counter() - tb
-        if rank != 0:
+        if rank != 0 or world == 1:  # (one rank: rank 0 projects with the received image too)
             info = nat.ProjectorInfo()
             for f in ("m", "p", "nnz", "layout", "value_type", "magnitude", "block_shift", "n_buffers"):
                 setattr(info, f, meta[f])
@@ -257,18 +262,19 @@ def main():
     nnz_a = int(Aj.numel())
     log(f"[rank {rank}] A: {args.rows} rows, nnz={nnz_a} ({time.perf_counter() - t0:.1f}s)")
 
-    if world > 1:
+    if pg:
         ranks_seen = dist.get_world_size()
         if ranks_seen != world:
             raise RuntimeError(f"process group has {ranks_seen} ranks, --gpus {world}")
-    args.dist_info = {"ranks_seen": dist.get_world_size() if world > 1 else 1,
-                      "backend": dist.get_backend() if world > 1 else None,
-                      "r_broadcast_ms": t_bcast * 1e3, "rehearsal_one_gpu": rehearse}
-    args.r_meta = meta if world > 1 else None
+    args.dist_info = {"ranks_seen": dist.get_world_size() if pg else 1,
+                      "backend": dist.get_backend() if pg else None,
+                      "r_broadcast_ms": t_bcast * 1e3, "rehearsal_one_gpu": rehearse,
+                      "r_from_broadcast_image": bool(pg)}
+    args.r_meta = meta if pg else None
     if args.boundary in ("host", "libsvm", "partition"):
         {"host": bench_host, "libsvm": bench_libsvm, "partition": bench_partition}[args.boundary](
             args, cfg, P, R_host, Ap, Aj, Ax, world, rank, dev)
-        if world > 1:
+        if pg:
             dist.destroy_process_group()
         return
 
@@ -278,6 +284,7 @@ def main():
         P.set_staging(args.staging, args.stage_shift)
     if args.pipeline != "auto":
         P.set_option("pipeline", args.pipeline)
+    P.set_option("lpr_split", args.lpr_split)
     try:  # full workspace (deferred tile output + staging); the minimal one if HBM is short
         ws = torch.empty(P.workspace_bytes(args.rows, nnz_a, dtype=Ax.dtype), dtype=torch.uint8, device=dev)
     except torch.OutOfMemoryError:
@@ -309,7 +316,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -320,7 +327,7 @@ def main():
     e1.record(torch.cuda.current_stream(dev))
     torch.cuda.synchronize()
     t_wall = time.perf_counter() - t0
-    if world > 1:
+    if pg:
         dist.barrier()
     kernel_ms = e0.elapsed_time(e1) / args.steps
     staged_run = P.choice(args.rows, nnz_a, ws)  # auto mode: what the device chose for these rows
@@ -412,7 +419,7 @@ def main():
             "tiles": n_tiles_run, "deferred_tiles": n_deferred, "staged_this_call": staged_run,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

@@ -95,9 +95,14 @@ int inclusive_scan_i64(int64_t* a, int64_t n, hipStream_t st, DevBuf& tmp, int d
 // Same contract as rp_libsvm_parse_device, on stream st.
 struct LibsvmScratch {
     DevBuf counts, tmp, nl, keep, items, errb, slow;
+    // the line structure of the last text counted into this scratch (newline positions, kept-line
+    // and item prefix sums): a call with reuse_counts parses that same text without counting again
+    bool counted = false;
+    int64_t n_nl = 0, n_lines = 0, rows = 0, total = 0, bytes = -1;
 };
 int libsvm_parse(LibsvmScratch& s, int device, const char* text, int64_t n_bytes, int64_t num_features,
                  double* labels, void* indptr, int32_t indptr_type, int32_t* indices, float* data, int64_t cap_rows,
-                 int64_t cap_nnz, hipStream_t st, int64_t* n_rows, int64_t* nnz, int64_t* err_line);
+                 int64_t cap_nnz, hipStream_t st, int64_t* n_rows, int64_t* nnz, int64_t* err_line,
+                 bool reuse_counts = false);
 
 }  // namespace rpd

@@ -634,7 +634,7 @@ const char* reason(int c) {
 int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n_bytes, int64_t num_features,
                       double* labels, void* indptr, int32_t indptr_type, int32_t* indices, float* data,
                       int64_t cap_rows, int64_t cap_nnz, hipStream_t st, int64_t* n_rows, int64_t* nnz,
-                      int64_t* err_line) {
+                      int64_t* err_line, bool reuse_counts) {
     if (!n_rows || !nnz || n_bytes < 0 || (n_bytes > 0 && !text)) return fail(RP_ERR_INVALID, "bad argument");
     if (indptr && indptr_type != RP_I32 && indptr_type != RP_I64) return fail(RP_ERR_INVALID, "bad indptr type");
     if (err_line) *err_line = -1;
@@ -645,47 +645,66 @@ int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n
     DevBuf &counts = sc.counts, &tmp = sc.tmp, &nl = sc.nl, &keep = sc.keep, &items = sc.items, &errb = sc.errb,
            &slow = sc.slow;
     int rc;
-    if ((rc = counts.ensure(8 * (size_t)nblk, device))) return rc;
-    hipLaunchKernelGGL(nl_count_kernel, dim3((unsigned)nblk), dim3(kLB), 0, st, t, n_bytes, (int64_t*)counts.p);
-    HIP_TRY(hipGetLastError());
-    if ((rc = inclusive_scan_i64((int64_t*)counts.p, nblk, st, tmp, device))) return rc;
-    int64_t n_nl = 0;
-    HIP_TRY(hipMemcpyAsync(&n_nl, (int64_t*)counts.p + nblk - 1, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    unsigned char last = '\n';
-    if (n_bytes > 0) {
-        HIP_TRY(hipMemcpyAsync(&last, t + n_bytes - 1, 1, hipMemcpyDeviceToHost, st));
+    int64_t n_nl = 0, n_lines = 0, rows = 0, total = 0;
+    auto count = [&]() -> int {  // newline positions, kept lines, items per line (prefix sums)
+        if ((rc = counts.ensure(8 * (size_t)nblk, device))) return rc;
+        hipLaunchKernelGGL(nl_count_kernel, dim3((unsigned)nblk), dim3(kLB), 0, st, t, n_bytes, (int64_t*)counts.p);
+        HIP_TRY(hipGetLastError());
+        if ((rc = inclusive_scan_i64((int64_t*)counts.p, nblk, st, tmp, device))) return rc;
+        HIP_TRY(hipMemcpyAsync(&n_nl, (int64_t*)counts.p + nblk - 1, 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        unsigned char last = '\n';
+        if (n_bytes > 0) {
+            HIP_TRY(hipMemcpyAsync(&last, t + n_bytes - 1, 1, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+        }
+        n_lines = n_nl + (last != '\n' ? 1 : 0);
+        if ((rc = nl.ensure(8 * (size_t)std::max<int64_t>(n_nl, 1), device))) return rc;
+        if (n_nl > 0) {
+            hipLaunchKernelGGL(nl_mark_kernel, dim3((unsigned)nblk), dim3(kLB), 0, st, t, n_bytes,
+                               (const int64_t*)counts.p, (int64_t*)nl.p);
+            HIP_TRY(hipGetLastError());
+        }
+        if ((rc = keep.ensure(8 * (size_t)(n_lines + 1), device)) || (rc = items.ensure(8 * (size_t)(n_lines + 1), device)) ||
+            (rc = errb.ensure(16, device)))
+            return rc;
+        HIP_TRY(hipMemsetAsync(keep.p, 0, 8, st));
+        HIP_TRY(hipMemsetAsync(items.p, 0, 8, st));
+        HIP_TRY(hipMemsetAsync(errb.p, 0xff, 8, st));
+        HIP_TRY(hipMemsetAsync((char*)errb.p + 8, 0, 8, st));  // lines for the exact slow path
+        if (n_lines > 0) {
+            const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_lines + 255) / 256, 1), 65536);
+            hipLaunchKernelGGL(line_count_kernel, dim3(grid), dim3(256), 0, st, t, n_bytes, (const int64_t*)nl.p, n_nl,
+                               n_lines, (int64_t*)keep.p, (int64_t*)items.p);
+            HIP_TRY(hipGetLastError());
+            if ((rc = inclusive_scan_i64((int64_t*)keep.p + 1, n_lines, st, tmp, device))) return rc;
+            if ((rc = inclusive_scan_i64((int64_t*)items.p + 1, n_lines, st, tmp, device))) return rc;
+        }
+        HIP_TRY(hipMemcpyAsync(&rows, (int64_t*)keep.p + n_lines, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&total, (int64_t*)items.p + n_lines, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        sc.counted = true;
+        sc.n_nl = n_nl;
+        sc.n_lines = n_lines;
+        sc.rows = rows;
+        sc.total = total;
+        sc.bytes = n_bytes;
+        return RP_OK;
+    };
+    if (reuse_counts && sc.counted && sc.bytes == n_bytes) {  // the same text, counted by the call before
+        n_nl = sc.n_nl;
+        n_lines = sc.n_lines;
+        rows = sc.rows;
+        total = sc.total;
+    } else {
+        sc.counted = false;
+        if ((rc = count())) return rc;
     }
-    const int64_t n_lines = n_nl + (last != '\n' ? 1 : 0);
-    if ((rc = nl.ensure(8 * (size_t)std::max<int64_t>(n_nl, 1), device))) return rc;
-    if (n_nl > 0) {
-        hipLaunchKernelGGL(nl_mark_kernel, dim3((unsigned)nblk), dim3(kLB), 0, st, t, n_bytes,
-                           (const int64_t*)counts.p, (int64_t*)nl.p);
-        HIP_TRY(hipGetLastError());
-    }
-    if ((rc = keep.ensure(8 * (size_t)(n_lines + 1), device)) || (rc = items.ensure(8 * (size_t)(n_lines + 1), device)) ||
-        (rc = errb.ensure(16, device)))
-        return rc;
-    HIP_TRY(hipMemsetAsync(keep.p, 0, 8, st));
-    HIP_TRY(hipMemsetAsync(items.p, 0, 8, st));
-    HIP_TRY(hipMemsetAsync(errb.p, 0xff, 8, st));
-    HIP_TRY(hipMemsetAsync((char*)errb.p + 8, 0, 8, st));  // lines for the exact slow path
     const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_lines + 255) / 256, 1), 65536);
-    if (n_lines > 0) {
-        hipLaunchKernelGGL(line_count_kernel, dim3(grid), dim3(256), 0, st, t, n_bytes, (const int64_t*)nl.p, n_nl,
-                           n_lines, (int64_t*)keep.p, (int64_t*)items.p);
-        HIP_TRY(hipGetLastError());
-        if ((rc = inclusive_scan_i64((int64_t*)keep.p + 1, n_lines, st, tmp, device))) return rc;
-        if ((rc = inclusive_scan_i64((int64_t*)items.p + 1, n_lines, st, tmp, device))) return rc;
-    }
-    int64_t rows = 0, total = 0;
-    HIP_TRY(hipMemcpyAsync(&rows, (int64_t*)keep.p + n_lines, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(&total, (int64_t*)items.p + n_lines, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
     *n_rows = rows;
     *nnz = total;  // upper bound until parsed: items counted; every parsed item is stored
     if (!indices) return RP_OK;
+    sc.counted = false;
     if (!labels || !indptr || !data) return fail(RP_ERR_INVALID, "NULL output buffer");
     if (rows > cap_rows || total > cap_nnz)
         return fail(RP_ERR_CAPACITY, "need %lld rows / %lld entries", (long long)rows, (long long)total);

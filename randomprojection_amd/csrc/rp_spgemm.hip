@@ -1093,7 +1093,7 @@ struct LprSpace {
     unsigned long long* off;  // 4 x n_tiles: exclusive prefix of cnt (+ base)
     uint32_t* hlist;      // heavy tiles, count in ws->n_deferred
     uint32_t* tflag;      // n_tiles: 1 = heavy (lpr_heavy_write places the tile)
-    uint32_t* rowmeta;    // n_tiles x 256: row's first slot position << 16 | row's entry count
+    uint32_t* rowmeta;    // n_tiles x 256: the row's offset in its wave's output run (lpr_store_rows)
     uint16_t* cols;       // 4 x n_tiles x slot
     unsigned char* vals;  // 4 x n_tiles x slot x sizeof(T)
     unsigned long long* scan_state;  // one per 4096-wave scan block
@@ -1101,6 +1101,41 @@ struct LprSpace {
 };
 
 __device__ __forceinline__ uint32_t lpr_h2(uint32_t col) { return (col * 0x9E3779B1u) >> 26; }
+
+// A wave's rows to HBM in their final order, back to back (row r's kept entries [kst, kst + kept)
+// of the LDS slot, reversed for scipy's reverse first-touch order or as built for RP_ORDER_SORTED;
+// gaps the exact path left between rows are squeezed out), so that the copy kernel moves one
+// contiguous run per wave. rowpre[lane] = the row's offset in the run, *cnt = the run's length.
+template <typename T>
+__device__ __forceinline__ void lpr_store_rows(const uint16_t* cb, const T* vb, uint32_t kst, uint32_t kept,
+                                               bool valid, int lane, int order, uint32_t* __restrict__ rowpre,
+                                               uint32_t* __restrict__ cnt, uint16_t* __restrict__ oc,
+                                               T* __restrict__ ov) {
+    const uint32_t c = valid ? kept : 0u;
+    const uint32_t inc = wave_scan_dpp(c);
+    const uint32_t pre = inc - c;
+    const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
+    if (valid) rowpre[lane] = pre;
+    if (lane == 0) *cnt = tot;
+    for (uint32_t o0 = 0; o0 < tot; o0 += 64) {  // wave-uniform trip count: every lane shuffles
+        const uint32_t o = o0 + lane;
+        // the row holding output o: the last lane whose prefix is <= o (empty rows before it share
+        // its prefix; rows after it start past o)
+        int lo = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t pv = __shfl(pre, lo + step, 64);
+            if (lo + step < 64 && pv <= o) lo += step;
+        }
+        const uint32_t rp = __shfl(pre, lo, 64), rk = __shfl(kst, lo, 64), rc = __shfl(c, lo, 64);
+        if (o < tot) {
+            const uint32_t i = o - rp;
+            const uint32_t src = order == RP_ORDER_SORTED ? rk + i : rk + rc - 1 - i;
+            __builtin_nontemporal_store(cb[src], oc + o);
+            __builtin_nontemporal_store(vb[src], ov + o);
+        }
+    }
+}
 
 // products of an entry with LDS descriptor d: bits 30-31 = n <= 2 inline 15-bit slots (sign << 14 |
 // col) in R's storage order; n = 3: the W word in side[d & mask] (<= 4 inline, or an O record).
@@ -1604,19 +1639,10 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
                         vb[b] = kv;
                     }
                 }
-                if (valid) sp.rowmeta[(size_t)tile * kLprRows + r] = (kst << 16) | kept;
-                const uint32_t wtot = __builtin_amdgcn_readlane(wave_scan_dpp(valid ? kept : 0u), 63);
-                if (lane == 0) sp.cnt[(size_t)tile * 4 + w] = wtot;
-                // the slot to HBM, coalesced (rows may end before their kept range when the exact
-                // path dropped entries: the whole used range goes, the copy kernel reads each row's
-                // own part)
                 __builtin_amdgcn_wave_barrier();
-                uint16_t* __restrict__ oc = sp.cols + ((size_t)tile * 4 + w) * sp.slot;
-                T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + ((size_t)tile * 4 + w) * sp.slot;
-                for (uint32_t q = lane; q < carry_k; q += 64) {
-                    oc[q] = cb[q];
-                    ov[q] = vb[q];
-                }
+                const size_t wt = (size_t)tile * 4 + w;
+                lpr_store_rows<T>(cb, vb, kst, kept, valid, lane, order, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
+                                  sp.cnt + wt, sp.cols + wt * sp.slot, reinterpret_cast<T*>(sp.vals) + wt * sp.slot);
             }
         }
         STAMP(5);
@@ -2029,18 +2055,10 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
             vb[b] = kv;
         }
     }
-    if (valid) sp.rowmeta[(size_t)tile * kLprRows + r] = (kst << 16) | kept;
-    const uint32_t wtot = __builtin_amdgcn_readlane(wave_scan_dpp(valid ? kept : 0u), 63);
-    if (lane == 0) sp.cnt[(size_t)tile * 4 + w] = wtot;
-    // the slot to HBM, coalesced (rows may end before their kept range when the exact path
-    // dropped entries: the whole used range goes, the copy kernel reads each row's own part)
     __builtin_amdgcn_wave_barrier();
-    uint16_t* __restrict__ oc = sp.cols + ((size_t)tile * 4 + w) * sp.slot;
-    T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + ((size_t)tile * 4 + w) * sp.slot;
-    for (uint32_t q = lane; q < carry_k; q += 64) {
-        oc[q] = cb[q];
-        ov[q] = vb[q];
-    }
+    const size_t wt = (size_t)tile * 4 + w;
+    lpr_store_rows<T>(cb, vb, kst, kept, valid, lane, order, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
+                      sp.cnt + wt, sp.cols + wt * sp.slot, reinterpret_cast<T*>(sp.vals) + wt * sp.slot);
     STAMP(4);
     STAMP(5);
     STAMP(6);
@@ -2155,7 +2173,10 @@ __device__ __forceinline__ uint32_t lpr_slot_de(uint32_t d, uint32_t t, const ui
 // row metadata, the slot stored coalesced.
 constexpr int kWaveSteps = 12;                 // flat-pass steps per load round (avg KDD2012: 11)
 constexpr int kWaveMaxSteps = 32;              // entries per unit beyond 32 x 64 -> heavy tile
-constexpr int kWaveSide = 32;                  // side entries per unit beyond this -> heavy tile
+// side entries (features with > 2 R entries, 1.9% of KDD2012's) per unit beyond this -> heavy tile.
+// Poisson tails: a 704-entry unit has 13.3 on average; 32 was exceeded by ~7 of 1.87M units per
+// configs[1] pass (4e-6 each), and 6 heavy tiles cost 1.6 ms; past 64: ~1e-24.
+constexpr int kWaveSide = 64;
 constexpr int kWaveScr = 128;                  // exact-path scratch (products of one row)
 __host__ __device__ inline size_t lpr_wave_lds_bytes(uint32_t slot, size_t vs) {
     return ((2 * (size_t)slot + 15) & ~size_t(15)) + ((vs * (size_t)slot + 15) & ~size_t(15)) +
@@ -2408,16 +2429,9 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             vb[b] = kv;
         }
     }
-    if (valid) sp.rowmeta[(size_t)row0 + lane] = (kst << 16) | kept;
-    const uint32_t wtot = __builtin_amdgcn_readlane(wave_scan_dpp(valid ? kept : 0u), 63);
-    if (lane == 0) sp.cnt[rb] = wtot;
     __builtin_amdgcn_wave_barrier();
-    uint16_t* __restrict__ oc = sp.cols + (size_t)rb * sp.slot;
-    T* __restrict__ ov = reinterpret_cast<T*>(sp.vals) + (size_t)rb * sp.slot;
-    for (uint32_t q = lane; q < carry_k; q += 64) {
-        oc[q] = cb[q];
-        ov[q] = vb[q];
-    }
+    lpr_store_rows<T>(cb, vb, kst, kept, valid, lane, order, sp.rowmeta + row0, sp.cnt + rb,
+                      sp.cols + (size_t)rb * sp.slot, reinterpret_cast<T*>(sp.vals) + (size_t)rb * sp.slot);
 }
 
 // heavy tiles, pass 0: the exact dense accumulator counts their rows (grid-stride over the list);
@@ -2507,12 +2521,13 @@ lpr_scan_kernel(LprSpace sp, size_t n, const unsigned long long* __restrict__ ba
     }
 }
 
-// slots -> C: one workgroup per tile (grid-stride), one wave per 64-row slot; rows reversed for
-// scipy's order (the slot holds first-touch order) or copied as they are (sorted in the slot)
+// runs -> C: one workgroup per tile (grid-stride), one wave per 64-row unit: the unit's run (rows
+// already in their final order, back to back: lpr_store_rows) copied to its offset, indptr from
+// the rows' offsets in the run. Heavy tiles are placed by lpr_heavy_write_kernel.
 template <typename T, typename OP, typename OI>
 __global__ void __launch_bounds__(kBlock)
 lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ Cp, OI* __restrict__ Cj,
-                T* __restrict__ Cx, unsigned long long capacity, int order) {
+                T* __restrict__ Cx, unsigned long long capacity) {
     const T* vals = reinterpret_cast<const T*>(sp.vals);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (unsigned tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -2523,32 +2538,14 @@ lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ 
         const int64_t row0 = (int64_t)tile * kLprRows;
         const int nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
         const int r = 64 * w + lane;
-        const uint32_t meta = r < nrows ? sp.rowmeta[(size_t)tile * kLprRows + r] : 0u;
-        const uint32_t c = meta & 0xffffu, src = meta >> 16;
-        const uint32_t inc = wave_incl_scan_t<uint32_t>(c, lane);
-        const uint32_t pre = inc - c;
-        if (r < nrows) Cp[row0 + r] = (OP)(G + pre);
+        if (r < nrows) Cp[row0 + r] = (OP)(G + sp.rowmeta[row0 + r]);
         if (tile == n_tiles - 1 && threadIdx.x == kBlock - 1) Cp[n_rows] = (OP)(G + cnt);
         if (G + cnt > capacity) continue;
-        const uint16_t* sc = sp.cols + wt * sp.slot;
-        const T* sv = vals + wt * sp.slot;
-        for (uint32_t o0 = 0; o0 < cnt; o0 += 64) {  // uniform trip count: every lane takes part in the shuffles
-            const uint32_t o = o0 + lane;
-            // the row holding output o: the last lane whose prefix is <= o (binary search)
-            int lo = 0;
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1) {
-                const uint32_t pv = __shfl(pre, lo + step, 64);
-                if (lo + step < 64 && pv <= o) lo += step;
-            }
-            // several empty rows share a prefix: the row that owns o is the last of them with c > 0
-            const uint32_t rp = __shfl(pre, lo, 64), rc = __shfl(c, lo, 64), rsrc = __shfl(src, lo, 64);
-            const uint32_t i = o - rp;
-            if (o < cnt) {
-                const uint32_t s = order == RP_ORDER_SORTED ? rsrc + i : rsrc + rc - 1 - i;
-                Cj[G + o] = (OI)sc[s];
-                Cx[G + o] = sv[s];
-            }
+        const uint16_t* __restrict__ sc = sp.cols + wt * sp.slot;
+        const T* __restrict__ sv = vals + wt * sp.slot;
+        for (uint32_t q = lane; q < cnt; q += 64) {
+            Cj[G + q] = (OI)__builtin_nontemporal_load(sc + q);
+            Cx[G + q] = __builtin_nontemporal_load(sv + q);
         }
     }
 }
@@ -3083,7 +3080,7 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL((lpr_copy_kernel<T, OP, OI>), dim3(std::min<unsigned>(n_tiles, 1u << 20)), dim3(kBlock), 0, st,
                        sp, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices, (T*)c->data,
-                       (unsigned long long)c->capacity, order);
+                       (unsigned long long)c->capacity);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipFuncSetAttribute((const void*)lpr_heavy_write_kernel<T, IP, OP, OI>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl));
@@ -4431,7 +4428,8 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
             (r = stream_alloc_slot(h, t.s, rows, nnz, cap, 8, 4, c->indptr_type, c->indices_type)))
             return r;
         r = libsvm_parse(t.ps, dev, (const char*)t.text.p, tc.bytes, h->m, (double*)t.labels.p, t.s.ap.p, RP_I64,
-                         (int32_t*)t.s.aj.p, (float*)t.s.ax.p, rows, nnz, st_comp, &rows, &nnz, &el);
+                         (int32_t*)t.s.aj.p, (float*)t.s.ax.p, rows, nnz, st_comp, &rows, &nnz, &el,
+                         /*reuse_counts=*/true);  // the count call just above: its line tables stand
         if (r == RP_ERR_INVALID && el >= 0) bad_line = lines_before(text, tc.b0) + el;
         if (r) return r;
         cks[(size_t)k].rows = rows;

@@ -143,3 +143,23 @@ def test_bench_gpus_two_launches_two_ranks():
     assert v["sample_bitexact_vs_oracle"] and v["indptr_ok"] and v["columns_ok"] and v["ranks_verified"] == 2
     assert line["cpu_baseline"] and line["cpu_baseline"]["value"] > 0
     assert line["librp"]["checked_against_sources"] and line["value"] > 0
+
+
+def test_bench_rccl_path_one_rank():
+    """The RCCL branch of bench.py executes on this one-GPU box (RP_BENCH_FORCE_PG=1 at world size 1):
+    init_process_group("nccl", device_id=...), the broadcast of R's packed device image over RCCL,
+    the projector rebuilt from the received image (rp_projector_create_from_device), barriers, and
+    the projection by that projector checked against the oracle — the code the 8-GPU driver run uses,
+    minus the peers."""
+    import json
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RP_BENCH_REHEARSE_ONE_GPU",)}
+    env.update(RP_BENCH_FORCE_PG="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_port()))
+    bench = os.path.join(os.path.dirname(HERE), "bench.py")
+    r = subprocess.run([sys.executable, bench, "--gpus", "1", "--rows", "1000000", "--m", "3000000", "--steps", "2",
+                        "--warmup", "1", "--no-cpu-baseline"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["backend"] == "nccl" and line["ranks_seen"] == 1 and line["r_from_broadcast_image"]
+    assert line["verified"]["sample_bitexact_vs_oracle"] and line["verified"]["indptr_ok"]
