@@ -859,7 +859,7 @@ __device__ __forceinline__ uint32_t run_of(const uint16_t* st, int nb, uint32_t 
 // words). S word: entry index in the tile << 20 | column bits. A run past its segment's reserve
 // sets the gate to 0: the call's remaining kernels take the direct path (lpr_main_flat_kernel). A
 // tile past the entry cap stages nothing (its counts are 0): the heavy path reads A itself.
-constexpr int kPartTiles = 4;
+constexpr int kPartTiles = 2;
 constexpr int kPBlock = kBlock * kPartTiles;
 static_assert(kRunGroup % kPartTiles == 0, "a super-tile never straddles two groups");
 template <typename IP>
@@ -909,11 +909,10 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
     __syncthreads();
     const uint32_t cnt = qt < nb ? s_cur[q][qt] : 0u;
     // the super-tile's claim of bucket qt (quarter 0): issued now, consumed after the ranking
-    uint32_t claim = 0, c4[kPartTiles] = {};
+    uint32_t claim = 0, c4[kPartTiles] = {}, tot4 = 0;
     int64_t lo = 0, hi = 0;
     const unsigned sg = (t0 / kRunGroup) * (unsigned)nb + (unsigned)qt;
     if (q == 0 && qt < nb) {
-        uint32_t tot4 = 0;
 #pragma unroll
         for (int k = 0; k < kPartTiles; ++k) {
             c4[k] = s_cur[k][qt];
@@ -951,7 +950,7 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
         }
     if (q == 0 && qt < nb) {  // the four tiles' runs of bucket qt, adjacent in tile order
         uint32_t run = claim;
-        if (c4[0] + c4[1] + c4[2] + c4[3] > 0 && lo + (int64_t)claim + c4[0] + c4[1] + c4[2] + c4[3] > hi) s_over = 1;
+        if (tot4 > 0 && lo + (int64_t)claim + tot4 > hi) s_over = 1;
 #pragma unroll
         for (int k = 0; k < kPartTiles; ++k) {
             if (t0 + k < n_tiles) {
