@@ -115,7 +115,7 @@ def step_kernels(plan, staged_run):
             ks = ["lpr_choose_kernel"] + ks
         return ks
     ks = ["spgemm_lookback_kernel", "defer_copy_kernel"]
-    return (["stage_partition_kernel", "stage_gather_kernel"] + ks) if plan["staged"] else ks
+    return (["filter_probe_kernel", "filter_kernel"] + ks) if plan["pipeline"] == "tile_filtered" else ks
 
 
 def algorithmic_bytes_per_row(a, rbar, c):
@@ -145,6 +145,8 @@ def main():
     ap.add_argument("--stage-shift", type=int, default=0, help="2^shift features per staging bucket (0 = auto)")
     ap.add_argument("--pipeline", choices=["auto", "tile", "rowlane"], default="auto",
                     help="force a kernel pipeline where it can run (results identical; measurements)")
+    ap.add_argument("--filter", type=int, choices=[-1, 0, 1], default=-1,
+                    help="tile pipeline: drop A entries with empty R rows first (-1 auto, 0 off, 1 on)")
     ap.add_argument("--lpr-split", type=int, choices=[-1, 0, 1], default=-1,
                     help="staged row-lane: 1 unsort + wave kernels (default), 0 the persistent main kernel")
     ap.add_argument("--cpu-sample-rows", type=int, default=None)
@@ -285,6 +287,7 @@ def main():
     if args.pipeline != "auto":
         P.set_option("pipeline", args.pipeline)
     P.set_option("lpr_split", args.lpr_split)
+    P.set_option("filter", args.filter)
     try:  # full workspace (deferred tile output + staging); the minimal one if HBM is short
         ws = torch.empty(P.workspace_bytes(args.rows, nnz_a, dtype=Ax.dtype), dtype=torch.uint8, device=dev)
     except torch.OutOfMemoryError:

@@ -176,29 +176,35 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
  *   RP_OPT_DEFER_TICKS   256-row tiles' look-back wait budget in s_memrealtime ticks (100 MHz):
  *                        -1 default (800 = 8 us); n >= 0 override
  *   RP_OPT_CHUNK_ROWS    row-lane rows per launch sequence: 0 default (2^27), else rounded up to
- *                        whole 256-row tiles
+ *                        whole 256-row tiles; also caps the filtered tile pipeline's rows per chunk
+ *                        (a cap below n_rows / 4096 makes that call run unfiltered)
  *   RP_OPT_HOST_THREADS  helper threads of the host result download: -1 default (min(4, cores));
  *                        0 or 1 plain copies
  *   RP_OPT_LPR_SPLIT     staged row-lane pipeline: -1 default (split), 1 split = unsort kernel +
- *                        barrier-free wave kernel, 0 the persistent main kernel */
+ *                        barrier-free wave kernel, 0 the persistent main kernel
+ *   RP_OPT_FILTER        tile pipeline over a packed R (m <= 2^26): 1 on — streaming passes first drop
+ *                        the A entries whose R row is empty (row chunks of <= 2^30 entries); -1 auto
+ *                        and 0 off (the default: measured slower on configs[3]) */
 typedef enum {
     RP_OPT_PIPELINE = 1,
     RP_OPT_DEFER_POLLS = 2,
     RP_OPT_DEFER_TICKS = 3,
     RP_OPT_CHUNK_ROWS = 4,
     RP_OPT_HOST_THREADS = 5,
-    RP_OPT_LPR_SPLIT = 6
+    RP_OPT_LPR_SPLIT = 6,
+    RP_OPT_FILTER = 7
 } rp_option;
 int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value);
 int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* value);
 
 /* The kernel pipeline rp_project_device would run for n_rows rows holding nnz_a entries with the
- * full workspace: *pipeline = RP_PIPE_TILE (one-launch tile SpGEMM with look-back) or
- * RP_PIPE_ROWLANE (row-lane kernel: short rows over a packed R), *staged = 1 if the R descriptors
+ * full workspace: *pipeline = RP_PIPE_TILE (one-launch tile SpGEMM with look-back),
+ * RP_PIPE_ROWLANE (row-lane kernel: short rows over a packed R) or RP_PIPE_TILE_FILTERED (the tile
+ * SpGEMM on A without its entries whose R row is empty, RP_OPT_FILTER), *staged = 1 if the R descriptors
  * are fetched by the staged gather, 0 if gathered directly, 2 if the device decides per call (auto
  * mode, rp_project_choice), *bucket_shift the staged bucket width (log2 features). Any out
  * pointer may be NULL. For logging and benchmarks; results are identical on every pipeline. */
-typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1 } rp_pipeline;
+typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1, RP_PIPE_TILE_FILTERED = 2 } rp_pipeline;
 int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t* pipeline, int32_t* staged,
                     int32_t* bucket_shift);
 

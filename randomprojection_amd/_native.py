@@ -16,6 +16,7 @@ RP_LAYOUT_AUTO, RP_LAYOUT_GENERIC, RP_LAYOUT_PACKED = 0, 1, 2
 RP_ORDER_SCIPY, RP_ORDER_SORTED = 0, 1
 RP_OPT_PIPELINE, RP_OPT_DEFER_POLLS, RP_OPT_DEFER_TICKS, RP_OPT_CHUNK_ROWS, RP_OPT_HOST_THREADS = 1, 2, 3, 4, 5
 RP_OPT_LPR_SPLIT = 6
+RP_OPT_FILTER = 7
 
 # every symbol include/rp.h declares (tests/test_abi.py checks the .so exports them all)
 EXPORTS = (
