@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <thread>
 
 #include "../../include/rp.h"
 
@@ -66,8 +67,31 @@ struct DevBuf {
         bytes = want;
         return RP_OK;
     }
+    // for buffers resized per chunk of a stream: 1/8 headroom, so sizes that drift up do not
+    // reallocate every chunk (hipFree / hipMalloc synchronise the whole device)
+    int grow(size_t n, int dev) { return n <= bytes && p ? RP_OK : ensure(n + n / 8, dev); }
 };
 
+
+// Waits of the streaming pipelines' threads: poll instead of hipStreamSynchronize /
+// hipEventSynchronize, which measured as serialising the other threads' HIP calls (a chunk's upload
+// started only once the compute stream drained: uploads and kernels did not overlap)
+inline hipError_t poll_event(hipEvent_t e) {
+    for (;;) {
+        const hipError_t r = hipEventQuery(e);
+        if (r != hipErrorNotReady) return r;
+        std::this_thread::yield();
+    }
+}
+inline hipError_t poll_stream(hipStream_t st) {
+    hipEvent_t e = nullptr;
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (r != hipSuccess) return r;
+    r = hipEventRecord(e, st);
+    if (r == hipSuccess) r = poll_event(e);
+    (void)hipEventDestroy(e);
+    return r;
+}
 
 inline int dtype_size(int t) {
     switch (t) {

@@ -647,26 +647,26 @@ int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n
     int rc;
     int64_t n_nl = 0, n_lines = 0, rows = 0, total = 0;
     auto count = [&]() -> int {  // newline positions, kept lines, items per line (prefix sums)
-        if ((rc = counts.ensure(8 * (size_t)nblk, device))) return rc;
+        if ((rc = counts.grow(8 * (size_t)nblk, device))) return rc;
         hipLaunchKernelGGL(nl_count_kernel, dim3((unsigned)nblk), dim3(kLB), 0, st, t, n_bytes, (int64_t*)counts.p);
         HIP_TRY(hipGetLastError());
         if ((rc = inclusive_scan_i64((int64_t*)counts.p, nblk, st, tmp, device))) return rc;
         HIP_TRY(hipMemcpyAsync(&n_nl, (int64_t*)counts.p + nblk - 1, 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(poll_stream(st));
         unsigned char last = '\n';
         if (n_bytes > 0) {
             HIP_TRY(hipMemcpyAsync(&last, t + n_bytes - 1, 1, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(poll_stream(st));
         }
         n_lines = n_nl + (last != '\n' ? 1 : 0);
-        if ((rc = nl.ensure(8 * (size_t)std::max<int64_t>(n_nl, 1), device))) return rc;
+        if ((rc = nl.grow(8 * (size_t)std::max<int64_t>(n_nl, 1), device))) return rc;
         if (n_nl > 0) {
             hipLaunchKernelGGL(nl_mark_kernel, dim3((unsigned)nblk), dim3(kLB), 0, st, t, n_bytes,
                                (const int64_t*)counts.p, (int64_t*)nl.p);
             HIP_TRY(hipGetLastError());
         }
-        if ((rc = keep.ensure(8 * (size_t)(n_lines + 1), device)) || (rc = items.ensure(8 * (size_t)(n_lines + 1), device)) ||
-            (rc = errb.ensure(16, device)))
+        if ((rc = keep.grow(8 * (size_t)(n_lines + 1), device)) || (rc = items.grow(8 * (size_t)(n_lines + 1), device)) ||
+            (rc = errb.grow(16, device)))
             return rc;
         HIP_TRY(hipMemsetAsync(keep.p, 0, 8, st));
         HIP_TRY(hipMemsetAsync(items.p, 0, 8, st));
@@ -682,7 +682,7 @@ int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n
         }
         HIP_TRY(hipMemcpyAsync(&rows, (int64_t*)keep.p + n_lines, 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(&total, (int64_t*)items.p + n_lines, 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(poll_stream(st));
         sc.counted = true;
         sc.n_nl = n_nl;
         sc.n_lines = n_lines;
@@ -711,7 +711,7 @@ int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n
     if (indptr_type == RP_I32 && total >= ((int64_t)1 << 31))
         return fail(RP_ERR_UNSUPPORTED, "nnz %lld needs int64 indptr", (long long)total);
     if (n_lines > 0) {
-        if ((rc = slow.ensure(8 * (size_t)n_lines, device))) return rc;
+        if ((rc = slow.grow(8 * (size_t)n_lines, device))) return rc;
         unsigned long long* ns = (unsigned long long*)errb.p + 1;
         const unsigned sgrid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_lines + 255) / 256, 1), 1024);
         if (indptr_type == RP_I64) {
@@ -742,7 +742,7 @@ int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n
     }
     unsigned long long e = 0;
     HIP_TRY(hipMemcpyAsync(&e, errb.p, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     if (e != ~0ull) {
         if (err_line) *err_line = (int64_t)(e >> 8);
         return fail(RP_ERR_INVALID, "libsvm line %lld: %s", (long long)(e >> 8), reason((int)(e & 0xff)));

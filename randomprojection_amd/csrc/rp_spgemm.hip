@@ -2896,20 +2896,28 @@ __global__ void scan_add_kernel(int64_t* a, int64_t n, const int64_t* bsum_scann
 }  // namespace
 
 namespace rpd {
+// block sums of every level in one scratch buffer (grown, never freed here: a hipFree per scan
+// synchronised the whole device and serialised the libsvm stream's uploads with its kernels)
+static int scan_level(int64_t* a, int64_t n, hipStream_t st, int64_t* scratch) {
+    const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
+    hipLaunchKernelGGL(scan_blocks_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, a, n, scratch);
+    if (nb > 1) {
+        scan_level(scratch, nb, st, scratch + nb + 1);
+        hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, a, n, scratch);
+    }
+    return RP_OK;
+}
+
 int inclusive_scan_i64(int64_t* a, int64_t n, hipStream_t st, DevBuf& tmp, int device) {
     if (n <= 0) return RP_OK;
-    const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
-    int rc = tmp.ensure(sizeof(int64_t) * (size_t)(nb + 1), device);
-    if (rc) return rc;
-    int64_t* bs = (int64_t*)tmp.p;
-    hipLaunchKernelGGL(scan_blocks_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, a, n, bs);
-    if (nb > 1) {
-        DevBuf tmp2;
-        rc = inclusive_scan_i64(bs, nb, st, tmp2, device);
-        if (rc) return rc;
-        hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)nb), dim3(kScanBlock), 0, st, a, n, bs);
-        HIP_TRY(hipStreamSynchronize(st));  // tmp2 freed at scope exit
+    size_t words = 0;
+    for (int64_t m = n; m > 1;) {
+        m = (m + kScanBlock - 1) / kScanBlock;
+        words += (size_t)m + 1;
     }
+    int rc = tmp.grow(sizeof(int64_t) * std::max<size_t>(words, 1), device);
+    if (rc) return rc;
+    scan_level(a, n, st, (int64_t*)tmp.p);
     HIP_TRY(hipGetLastError());
     return RP_OK;
 }
@@ -4374,6 +4382,7 @@ struct StreamSlot {
     DevBuf cp, cj, cx;        // output chunk: int64 chunk-relative indptr, int32 indices, values
     DevBuf optr, oidx;        // download forms: global indptr in the caller's type, int64 indices
     DevBuf ws, info;          // workspace; info = {base, nnz, first bad column pos, first bad row, error}
+    size_t ws_need = 0;       // workspace bytes this chunk's plan needs (<= ws.bytes)
     int64_t cap = 0;
     hipEvent_t comp = nullptr;
 };
@@ -4419,7 +4428,7 @@ int stream_upload(const rp_csr_in* a, const StreamChunk& ck, StreamSlot& s, hipS
         HIP_TRY(hipMemcpyAsync(s.ax.p, (const char*)a->data + (size_t)vs * ck.e0, (size_t)vs * ck.nnz,
                                hipMemcpyHostToDevice, st));
     }
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     return RP_OK;
 }
 
@@ -4450,7 +4459,7 @@ int stream_compute(rp_projector* h, const rp_csr_in* a, const StreamChunk& ck, S
     // before projecting (a short wait on this stream only; the copy threads keep going)
     unsigned long long chk[4];
     HIP_TRY(hipMemcpyAsync(chk, info, sizeof chk, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     if (chk[3] != ~0ull)
         return fail(RP_ERR_INVALID, "A indptr decreasing at row %lld", (long long)(ck.r0 + (int64_t)chk[3]));
     if (chk[2] != ~0ull)
@@ -4466,7 +4475,7 @@ int stream_project(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int or
     unsigned long long* info = (unsigned long long*)s.info.p;
     rp_csr_in ad{ck.rows, s.ap.p, RP_I64, (const int32_t*)s.aj.p, s.ax.p, vt, ck.nnz};
     rp_csr_out cd{s.cp.p, RP_I64, s.cj.p, RP_I32, s.cx.p, s.cap};
-    int rc = project_device_impl(h, &ad, &cd, order, s.ws.p, (int64_t)s.ws.bytes, st, nullptr, ck.nnz);
+    int rc = project_device_impl(h, &ad, &cd, order, s.ws.p, (int64_t)s.ws_need, st, nullptr, ck.nnz);
     if (rc) return rc;
     hipLaunchKernelGGL(stream_finish_kernel, dim3(1), dim3(64), 0, st, (const Workspace*)s.ws.p, total, info);
     const int64_t np = ck.rows + (last ? 1 : 0);  // the next chunk writes the shared boundary entry
@@ -4489,10 +4498,10 @@ int stream_project(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int or
 // download chunk results into the caller's arrays; *redo = entries did not fit the device slot
 int stream_download(const StreamChunk& ck, StreamSlot& s, const rp_csr_in* a, const rp_csr_out* c, bool last,
                     hipStream_t st, int vs, int64_t* nnz_out, bool* redo) {
-    HIP_TRY(hipEventSynchronize(s.comp));
+    HIP_TRY(poll_event(s.comp));
     unsigned long long info[5];
     HIP_TRY(hipMemcpyAsync(info, s.info.p, sizeof info, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     if (info[4]) return fail(RP_ERR_TIMEOUT, "device look-back wait expired (rows %lld..)", (long long)ck.r0);
     const int64_t base = (int64_t)info[0], k = (int64_t)info[1];
     *nnz_out = k;
@@ -4507,7 +4516,7 @@ int stream_download(const StreamChunk& ck, StreamSlot& s, const rp_csr_in* a, co
                                hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync((char*)c->data + (size_t)vs * base, s.cx.p, (size_t)vs * fit, hipMemcpyDeviceToHost, st));
     }
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     return RP_OK;
 }
 
@@ -4515,20 +4524,20 @@ int stream_alloc_slot(rp_projector* h, StreamSlot& s, int64_t rows, int64_t nnz,
                       int out_ip, int out_ix) {
     const int dev = h->device;
     int rc;
-    if ((rc = s.raw.ensure((size_t)ips * (rows + 1), dev)) || (rc = s.ap.ensure(8 * (size_t)(rows + 1), dev)) ||
-        (rc = s.aj.ensure(4 * (size_t)std::max<int64_t>(nnz, 1), dev)) ||
-        (rc = s.ax.ensure((size_t)vs * std::max<int64_t>(nnz, 1), dev)) ||
-        (rc = s.cp.ensure(8 * (size_t)(rows + 1), dev)) ||
-        (rc = s.cj.ensure(4 * (size_t)std::max<int64_t>(cap, 1), dev)) ||
-        (rc = s.cx.ensure((size_t)vs * std::max<int64_t>(cap, 1), dev)) ||
-        (rc = s.optr.ensure((size_t)dtype_size(out_ip) * (rows + 1), dev)) ||
-        (rc = s.info.ensure(64, dev)))
+    if ((rc = s.raw.grow((size_t)ips * (rows + 1), dev)) || (rc = s.ap.grow(8 * (size_t)(rows + 1), dev)) ||
+        (rc = s.aj.grow(4 * (size_t)std::max<int64_t>(nnz, 1), dev)) ||
+        (rc = s.ax.grow((size_t)vs * std::max<int64_t>(nnz, 1), dev)) ||
+        (rc = s.cp.grow(8 * (size_t)(rows + 1), dev)) ||
+        (rc = s.cj.grow(4 * (size_t)std::max<int64_t>(cap, 1), dev)) ||
+        (rc = s.cx.grow((size_t)vs * std::max<int64_t>(cap, 1), dev)) ||
+        (rc = s.optr.grow((size_t)dtype_size(out_ip) * (rows + 1), dev)) ||
+        (rc = s.info.grow(64, dev)))
         return rc;
-    if (out_ix == RP_I64 && (rc = s.oidx.ensure(8 * (size_t)std::max<int64_t>(cap, 1), dev))) return rc;
+    if (out_ix == RP_I64 && (rc = s.oidx.grow(8 * (size_t)std::max<int64_t>(cap, 1), dev))) return rc;
     const int64_t wsb = rp_project_workspace_bytes(h, rows, nnz);
     if (wsb < 0) return fail(RP_ERR_INVALID, "workspace size");
-    if ((rc = s.ws.ensure((size_t)wsb, dev))) return rc;
-    s.ws.bytes = (size_t)wsb;
+    if ((rc = s.ws.grow((size_t)wsb, dev))) return rc;
+    s.ws_need = (size_t)wsb;
     s.cap = cap;
     return RP_OK;
 }
@@ -4616,7 +4625,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
             StreamSlot& s = slots[k % ns];
             // the slot's input is free once chunk k - ns's kernels have run
             if (!sy.wait([&] { return sy.launched >= k - ns + 1 || k < ns; })) return;
-            if (k >= ns && hipEventSynchronize(s.comp) != hipSuccess)
+            if (k >= ns && poll_event(s.comp) != hipSuccess)
                 return sy.set_error(fail(RP_ERR_HIP, "event sync (upload)"));
             if (int r = stream_upload(a, chunks[(size_t)k], s, st_up, ips, vs)) return sy.set_error(r);
             sy.bump(sy.uploaded);
@@ -4782,9 +4791,9 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
     int64_t bad_line = -1;
     auto upload = [&](int64_t k, TextSlot& t) -> int {
         const TextChunk& tc = chunks[(size_t)k];
-        if (int r = t.text.ensure((size_t)tc.bytes + 16, dev)) return r;
+        if (int r = t.text.grow((size_t)tc.bytes + 16, dev)) return r;
         HIP_TRY(hipMemcpyAsync(t.text.p, text + tc.b0, (size_t)tc.bytes, hipMemcpyHostToDevice, st_up));
-        HIP_TRY(hipStreamSynchronize(st_up));
+        HIP_TRY(poll_stream(st_up));
         return RP_OK;
     };
     // parse chunk k in slot t (on st_comp) into t.s.ap/aj/ax and t.labels; fills cks[k] but r0
@@ -4795,7 +4804,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
                              nullptr, 0, 0, st_comp, &rows, &nnz, &el);
         if (r) return r;
         const int64_t cap = cap_out >= 0 ? cap_out : out_cap(nnz);
-        if ((r = t.labels.ensure(8 * (size_t)std::max<int64_t>(rows, 1), dev)) ||
+        if ((r = t.labels.grow(8 * (size_t)std::max<int64_t>(rows, 1), dev)) ||
             (r = stream_alloc_slot(h, t.s, rows, nnz, cap, 8, 4, c->indptr_type, c->indices_type)))
             return r;
         r = libsvm_parse(t.ps, dev, (const char*)t.text.p, tc.bytes, h->m, (double*)t.labels.p, t.s.ap.p, RP_I64,
@@ -4810,7 +4819,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
     };
     auto download = [&](int64_t k, TextSlot& t, int64_t* kn, bool* rd) -> int {
         const StreamChunk& ck = cks[(size_t)k];
-        HIP_TRY(hipEventSynchronize(t.s.comp));
+        HIP_TRY(poll_event(t.s.comp));
         if (ck.rows > 0)
             HIP_TRY(hipMemcpyAsync(labels + ck.r0, t.labels.p, 8 * (size_t)ck.rows, hipMemcpyDeviceToHost, st_down));
         return stream_download(ck, t.s, nullptr, c, k == K - 1, st_down, 4, kn, rd);
@@ -4820,7 +4829,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
         for (int64_t k = 0; k < K; ++k) {
             TextSlot& t = slots[k % ns];
             if (!sy.wait([&] { return sy.launched >= k - ns + 1 || k < ns; })) return;
-            if (k >= ns && hipEventSynchronize(t.s.comp) != hipSuccess)
+            if (k >= ns && poll_event(t.s.comp) != hipSuccess)
                 return sy.set_error(fail(RP_ERR_HIP, "event sync (upload)"));
             if (int r = upload(k, t)) return sy.set_error(r);
             sy.bump(sy.uploaded);
@@ -4939,7 +4948,7 @@ int rp_synth_rows_device(int device, int64_t n_rows, int64_t m, double mean_extr
     if (rc) return rc;
     int64_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, (int64_t*)ptr64.p + n_rows, 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     if (indptr_type == RP_I32 && total >= ((int64_t)1 << 31))
         return fail(RP_ERR_UNSUPPORTED, "nnz %lld needs int64 indptr", (long long)total);
     if (indptr_type == RP_I64) {
@@ -4959,7 +4968,7 @@ int rp_synth_rows_device(int device, int64_t n_rows, int64_t m, double mean_extr
                            perm_a, perm_b, (const int64_t*)ptr64.p, indices, data);
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(poll_stream(st));
     *nnz = total;
     return RP_OK;
 }
