@@ -13,7 +13,8 @@
 // next (features.values.astype(np.float32), clustermode/randomProjection.py:38). Labels stay f64.
 //
 // Kernels: newline count/mark per 4 KiB block (16 B per lane loads), one thread per line for
-// tokenising/counting and for parsing. Every literal Double.parseDouble accepts converts correctly
+// counting items (16-byte words, SWAR space masks), and a workgroup-cooperative parser (lines staged
+// in LDS, one thread per token; coop_parse_kernel). Every literal Double.parseDouble accepts converts correctly
 // rounded: Clinger's fast path, Eisel-Lemire for any exponent, hex literals, and an exact
 // decimal-shifting slow path (slow_line_kernel) for the rare long literals the first two cannot
 // settle.
@@ -582,23 +583,195 @@ __device__ int parse_line(const unsigned char* __restrict__ t, int64_t n, const 
     return code;
 }
 
+// error key of the first failure: line, then the failing item's rank in the line (0 = the label),
+// then the code; the smallest key is what a sequential parse meets first
+__device__ __forceinline__ unsigned long long err_key(int64_t line, uint32_t rank, int code) {
+    return ((unsigned long long)line << 20) | ((unsigned long long)std::min<uint32_t>(rank, 4095u) << 8) |
+           (unsigned long long)code;
+}
+
+// Workgroup-cooperative parse (the default). Workgroup b owns the lines that START in text bytes
+// [b kPB, (b + 1) kPB) and stages them whole into LDS with 16-byte loads; token starts (a byte other
+// than ' ' / '\n' after one of them) and newlines are counted per thread slice, block-scanned, and
+// listed in LDS; then one thread per token parses it from LDS: the line's first token is its label,
+// the others "index:value" items stored at off_of[line] + rank. Order and range checks read the
+// neighbouring token's index after a barrier. A block whose window holds other control bytes
+// (tab, CR), a token starting with '#' (comment lines), more than kWin bytes, kMaxTok tokens or
+// kMaxLn lines parses its lines one thread per line from global memory instead (parse_line).
+constexpr int kPB = 8192;             // text bytes per workgroup (two line-count blocks)
+constexpr int kWin = 12288;           // staged window: the block's lines, whole
+constexpr int kMaxTok = 2048, kMaxLn = 512;
+
 template <typename IP>
-__global__ void line_parse_kernel(const unsigned char* __restrict__ t, int64_t n,
-                                  const int64_t* __restrict__ nl_pos, int64_t n_nl, int64_t n_lines,
-                                  const int64_t* __restrict__ row_of, const int64_t* __restrict__ off_of,
-                                  int64_t num_features, double* __restrict__ labels, IP* __restrict__ indptr,
-                                  int32_t* __restrict__ indices, float* __restrict__ data,
-                                  unsigned long long* __restrict__ err, unsigned long long* __restrict__ n_slow,
-                                  int64_t* __restrict__ slow_lines) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n_lines;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        if (row_of[i + 1] == row_of[i]) continue;  // blank or comment line
-        bool slow = false;
-        const int code = parse_line<IP, false>(t, n, nl_pos, n_nl, i, row_of, off_of, num_features, labels, indptr,
-                                               indices, data, &slow);
-        if (code) atomicMin(err, ((unsigned long long)i << 8) | (unsigned long long)code);
-        else if (slow) slow_lines[atomicAdd(n_slow, 1ull)] = i;
+__global__ void __launch_bounds__(kLB)
+coop_parse_kernel(const unsigned char* __restrict__ t, int64_t n, const int64_t* __restrict__ counts,
+                  const int64_t* __restrict__ nl_pos, int64_t n_nl, int64_t n_lines,
+                  const int64_t* __restrict__ row_of, const int64_t* __restrict__ off_of, int64_t num_features,
+                  double* __restrict__ labels, IP* __restrict__ indptr, int32_t* __restrict__ indices,
+                  float* __restrict__ data, unsigned long long* __restrict__ err,
+                  unsigned long long* __restrict__ n_slow, int64_t* __restrict__ slow_lines) {
+    __shared__ __align__(16) unsigned char s_txt[kWin + 32];
+    __shared__ uint16_t s_tok[kMaxTok], s_tln[kMaxTok];
+    __shared__ int32_t s_j[kMaxTok];
+    __shared__ uint8_t s_code[kMaxTok];
+    __shared__ uint16_t s_lfirst[kMaxLn];
+    __shared__ uint32_t s_lslow[kMaxLn];
+    __shared__ uint32_t s_w[2][kLB / 64];
+    __shared__ int s_bad;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t B0 = (int64_t)blockIdx.x * kPB, B1 = std::min<int64_t>(n, B0 + kPB);
+    if (B0 >= n) return;
+    auto nl_lt = [&](int64_t x) -> int64_t {  // newlines before byte x (x a multiple of 4096, or n)
+        return x >= n ? n_nl : (x == 0 ? 0 : counts[x / kBytesPerBlock - 1]);
+    };
+    const int64_t i0 = B0 == 0 ? 0 : nl_lt(B0) - (t[B0 - 1] == '\n' ? 1 : 0) + 1;
+    const int64_t i1 = std::min<int64_t>(n_lines, nl_lt(B1) - (t[B1 - 1] == '\n' ? 1 : 0) + 1);
+    if (i0 >= i1) return;  // uniform
+    const int64_t S = i0 == 0 ? 0 : nl_pos[i0 - 1] + 1;
+    const int64_t E = i1 - 1 < n_nl ? nl_pos[i1 - 1] + 1 : n;
+    const int64_t W64 = E - S;
+    const int nlines = (int)(i1 - i0);
+    auto fallback = [&]() {
+        for (int64_t i = i0 + tid; i < i1; i += kLB) {
+            if (row_of[i + 1] == row_of[i]) continue;  // blank or comment line
+            bool slow = false;
+            const int code = parse_line<IP, false>(t, n, nl_pos, n_nl, i, row_of, off_of, num_features, labels,
+                                                   indptr, indices, data, &slow);
+            if (code) atomicMin(err, err_key(i, 0, code));
+            else if (slow) slow_lines[atomicAdd(n_slow, 1ull)] = i;
+        }
+    };
+    if (W64 > kWin || nlines > kMaxLn) {  // uniform
+        fallback();
+        return;
     }
+    const int W = (int)W64;
+    const int64_t a0 = S & ~int64_t(15);
+    const int o0 = (int)(S - a0);
+    const int nw = (int)((((E + 15) & ~int64_t(15)) - a0) / 16);
+    for (int w = tid; w < nw; w += kLB)
+        *reinterpret_cast<uint4*>(s_txt + 16 * w) = *reinterpret_cast<const uint4*>(t + a0 + 16 * w);
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    const unsigned char* b = s_txt + o0;
+    const int per = (W + kLB - 1) / kLB, p0 = std::min(W, tid * per), p1 = std::min(W, p0 + per);
+    auto is_sep = [](unsigned char c) { return c == ' ' || c == '\n'; };
+    uint32_t ntok = 0, nnl = 0;
+    bool bad = false;
+    {
+        bool prev = p0 == 0 || is_sep(b[p0 - 1]);
+        for (int p = p0; p < p1; ++p) {
+            const unsigned char c = b[p];
+            const bool sp = is_sep(c);
+            bad |= c < ' ' && c != '\n';
+            if (!sp && prev) {
+                ++ntok;
+                bad |= c == '#';
+            }
+            nnl += c == '\n';
+            prev = sp;
+        }
+    }
+    if (bad) s_bad = 1;
+    // block exclusive scan of (tokens, newlines) over the thread slices, in text order
+    uint32_t it = ntok, il = nnl;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t yt = __shfl_up(it, o, 64), yl = __shfl_up(il, o, 64);
+        if (lane >= o) { it += yt; il += yl; }
+    }
+    if (lane == 63) { s_w[0][wv] = it; s_w[1][wv] = il; }
+    __syncthreads();
+    uint32_t tb = it - ntok, lb = il - nnl, T = 0;
+#pragma unroll
+    for (int q = 0; q < kLB / 64; ++q) {
+        if (q < wv) { tb += s_w[0][q]; lb += s_w[1][q]; }
+        T += s_w[0][q];
+    }
+    if (s_bad || T > (uint32_t)kMaxTok) {  // uniform
+        fallback();
+        return;
+    }
+    {
+        bool prev = p0 == 0 || is_sep(b[p0 - 1]);
+        uint32_t k = tb, L = lb;
+        for (int p = p0; p < p1; ++p) {
+            const unsigned char c = b[p];
+            const bool sp = is_sep(c);
+            if (!sp && prev) {
+                s_tok[k] = (uint16_t)p;
+                s_tln[k] = (uint16_t)L;
+                ++k;
+            }
+            L += c == '\n';
+            prev = sp;
+        }
+    }
+    for (int L = tid; L < nlines; L += kLB) s_lslow[L] = 0u;
+    __syncthreads();
+    for (uint32_t k = tid; k < T; k += kLB)
+        if (k == 0 || s_tln[k - 1] != s_tln[k]) s_lfirst[s_tln[k]] = (uint16_t)k;
+    __syncthreads();
+    // one thread per token
+    for (uint32_t k = tid; k < T; k += kLB) {
+        const int p = s_tok[k];
+        int q = p;
+        while (q < W && !is_sep(b[q])) ++q;
+        const int L = s_tln[k];
+        const int64_t i = i0 + L;
+        const int64_t row = row_of[i];
+        const uint32_t f = s_lfirst[L];
+        int ok = 1;
+        if (f == k) {  // the label
+            const double lab = parse_double(b + p, b + q, &ok);
+            labels[row] = lab;
+            indptr[row] = (IP)off_of[i];
+            if (ok == 3) atomicOr(&s_lslow[L], 1u);
+            if (ok == 0) atomicMin(err, err_key(i, 0, E_LABEL));
+            s_code[k] = 0;
+            continue;
+        }
+        const int64_t out = off_of[i] + (k - f - 1);
+        int c1 = p;
+        while (c1 < q && b[c1] != ':') ++c1;
+        int c2 = c1 < q ? c1 + 1 : q;
+        while (c2 < q && b[c2] != ':') ++c2;
+        int code = 0;
+        int64_t idx = 0;
+        if (c1 >= q || c2 == c1 + 1) {
+            code = E_NOVALUE;
+        } else if (!parse_int(b + p, b + c1, &idx)) {
+            code = E_INDEX;
+        } else {
+            const double v = parse_double(b + c1 + 1, b + c2, &ok);
+            if (ok == 0) {
+                code = E_VALUE;
+            } else {
+                if (ok == 3) atomicOr(&s_lslow[L], 1u);
+                const int64_t j = idx - 1;
+                s_j[k] = (int32_t)std::max<int64_t>(std::min<int64_t>(j, INT32_MAX), -1);
+                indices[out] = (int32_t)j;
+                data[out] = (float)v;  // double -> float32 rounding, as features.values.astype(np.float32)
+            }
+        }
+        s_code[k] = (uint8_t)code;
+    }
+    __syncthreads();
+    // order (first) and range checks against the item before, errors keyed by (line, rank)
+    for (uint32_t k = tid; k < T; k += kLB) {
+        const int L = s_tln[k];
+        const uint32_t f = s_lfirst[L];
+        if (f == k) continue;
+        int code = s_code[k];
+        if (code == 0) {
+            const int64_t j = s_j[k], prevj = k - 1 == f ? -1 : s_j[k - 1];
+            if (j <= prevj) code = E_ORDER;
+            else if (j >= num_features) code = E_RANGE;
+        }
+        if (code) atomicMin(err, err_key(i0 + L, k - f, code));
+    }
+    for (int L = tid; L < nlines; L += kLB)
+        if (s_lslow[L]) slow_lines[atomicAdd(n_slow, 1ull)] = i0 + L;
 }
 
 // lines holding a literal the fast parser could not settle: parsed again, every literal exact
@@ -700,7 +873,6 @@ int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n
         sc.counted = false;
         if ((rc = count())) return rc;
     }
-    const unsigned grid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_lines + 255) / 256, 1), 65536);
     *n_rows = rows;
     *nnz = total;  // upper bound until parsed: items counted; every parsed item is stored
     if (!indices) return RP_OK;
@@ -714,19 +886,20 @@ int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n
         if ((rc = slow.grow(8 * (size_t)n_lines, device))) return rc;
         unsigned long long* ns = (unsigned long long*)errb.p + 1;
         const unsigned sgrid = (unsigned)std::min<int64_t>(std::max<int64_t>((n_lines + 255) / 256, 1), 1024);
+        const unsigned pgrid = (unsigned)std::max<int64_t>((n_bytes + kPB - 1) / kPB, 1);
         if (indptr_type == RP_I64) {
-            hipLaunchKernelGGL((line_parse_kernel<int64_t>), dim3(grid), dim3(256), 0, st, t, n_bytes,
-                               (const int64_t*)nl.p, n_nl, n_lines, (const int64_t*)keep.p, (const int64_t*)items.p,
-                               num_features, labels, (int64_t*)indptr, indices, data, (unsigned long long*)errb.p,
-                               ns, (int64_t*)slow.p);
+            hipLaunchKernelGGL((coop_parse_kernel<int64_t>), dim3(pgrid), dim3(kLB), 0, st, t, n_bytes,
+                               (const int64_t*)counts.p, (const int64_t*)nl.p, n_nl, n_lines, (const int64_t*)keep.p,
+                               (const int64_t*)items.p, num_features, labels, (int64_t*)indptr, indices, data,
+                               (unsigned long long*)errb.p, ns, (int64_t*)slow.p);
             hipLaunchKernelGGL((slow_line_kernel<int64_t>), dim3(sgrid), dim3(64), 0, st, t, n_bytes,
                                (const int64_t*)nl.p, n_nl, (const int64_t*)keep.p, (const int64_t*)items.p,
                                num_features, labels, (int64_t*)indptr, indices, data, ns, (const int64_t*)slow.p);
         } else {
-            hipLaunchKernelGGL((line_parse_kernel<int32_t>), dim3(grid), dim3(256), 0, st, t, n_bytes,
-                               (const int64_t*)nl.p, n_nl, n_lines, (const int64_t*)keep.p, (const int64_t*)items.p,
-                               num_features, labels, (int32_t*)indptr, indices, data, (unsigned long long*)errb.p,
-                               ns, (int64_t*)slow.p);
+            hipLaunchKernelGGL((coop_parse_kernel<int32_t>), dim3(pgrid), dim3(kLB), 0, st, t, n_bytes,
+                               (const int64_t*)counts.p, (const int64_t*)nl.p, n_nl, n_lines, (const int64_t*)keep.p,
+                               (const int64_t*)items.p, num_features, labels, (int32_t*)indptr, indices, data,
+                               (unsigned long long*)errb.p, ns, (int64_t*)slow.p);
             hipLaunchKernelGGL((slow_line_kernel<int32_t>), dim3(sgrid), dim3(64), 0, st, t, n_bytes,
                                (const int64_t*)nl.p, n_nl, (const int64_t*)keep.p, (const int64_t*)items.p,
                                num_features, labels, (int32_t*)indptr, indices, data, ns, (const int64_t*)slow.p);
@@ -744,8 +917,8 @@ int rpd::libsvm_parse(LibsvmScratch& sc, int device, const char* text, int64_t n
     HIP_TRY(hipMemcpyAsync(&e, errb.p, 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(poll_stream(st));
     if (e != ~0ull) {
-        if (err_line) *err_line = (int64_t)(e >> 8);
-        return fail(RP_ERR_INVALID, "libsvm line %lld: %s", (long long)(e >> 8), reason((int)(e & 0xff)));
+        if (err_line) *err_line = (int64_t)(e >> 20);
+        return fail(RP_ERR_INVALID, "libsvm line %lld: %s", (long long)(e >> 20), reason((int)(e & 0xff)));
     }
     return RP_OK;
 }

@@ -221,3 +221,61 @@ def test_project_text_stream_errors():
     with pytest.raises(nat.RPError) as c:
         project_text_stream(good.encode(), P, chunk_bytes=4096, out=small)
     assert c.value.code == nat.RP_ERR_CAPACITY
+
+
+# ---- the workgroup-cooperative parser (rp_libsvm.hip coop_parse_kernel): texts without tabs or
+# comments, so every 8 KB block is parsed one thread per token from LDS (a block holding a tab, a
+# '#' token or a window past 12 KB is parsed one thread per line instead)
+WHY = {"label is not a number": "label", "feature index is not an int": "index", "item without ':value'": "novalue",
+       "feature value is not a number": "value", "indices should be one-based and in ascending order": "order",
+       "feature index >= numFeatures": "range"}
+
+
+def spaced_text(rng, n, m, long_every=0):
+    """Lines with single and double separators, leading / trailing spaces, blank and all-space lines,
+    label-only lines; with ``long_every``, some lines of thousands of items (windows past 12 KB)."""
+    out = []
+    for i in range(n):
+        k = int(rng.integers(0, 25)) if not (long_every and i % long_every == long_every - 1) else 3000
+        idx = np.sort(rng.choice(m, size=k, replace=False)) + 1
+        items = [f"{j}:{v}" for j, v in zip(idx, rng.standard_normal(k).astype(np.float32))]
+        sep = "  " if i % 5 == 0 else " "
+        line = ["1", "0", "-1", "+1", "0.5", "3e0"][i % 6] + (sep + sep.join(items) if items else "")
+        if i % 9 == 0:
+            line = "   " + line + "  "
+        out.append(line)
+        if i % 23 == 0:
+            out.append("" if i % 2 else "    ")
+    return ("\n".join(out) + "\n").encode()
+
+
+@pytest.mark.parametrize("seed,long_every", [(10, 0), (11, 0), (12, 400)])
+def test_coop_parse_matches_oracle(seed, long_every):
+    rng = np.random.default_rng(seed)
+    m = 50_000
+    txt = spaced_text(rng, 6000, m, long_every)
+    assert b"\t" not in txt and b"#" not in txt
+    lab, ip, ix, vx = parse_text(txt, m)
+    labels, X = parse_bytes(txt, m)
+    assert same(labels, lab) and np.array_equal(X.indptr, ip) and np.array_equal(X.indices, ix)
+    assert same(X.data, vx)
+
+
+@pytest.mark.parametrize("bad", ["1 0:1", "1 3:1 3:2", "1 101:1", "x 1:1", "1 a:1", "1 3:", "1 3:x", "1 3:1 :2",
+                                 "1 3:x 2:1", "1 5:1 4:x", "1 2:1 1:1 200:1", "1 4:1 200:1 3:1", "1 2 3:1",
+                                 "y 1:x 0:1", "1 7:1 8:1 9:1 10:zz 5:1"])
+@pytest.mark.parametrize("where", [5, 700, 1999])
+def test_coop_errors_first_in_line_and_text(bad, where):
+    """The first error a sequential parse meets: the smallest line, and in it the leftmost failing
+    item, whatever the cooperative parser's thread order (a second bad line comes later)."""
+    rng = np.random.default_rng(where)
+    lines = spaced_text(rng, 2000, 100).decode().split("\n")[:-1]
+    lines[where] = bad
+    lines.insert(min(where + 50, len(lines)), "1 1:1 1:2")
+    txt = ("\n".join(lines) + "\n").encode()
+    with pytest.raises(ParseError) as ref:
+        parse_text(txt, 100)
+    with pytest.raises(LibsvmFormatError) as got:
+        parse_bytes(txt, 100)
+    assert got.value.line == ref.value.line == where
+    assert WHY[str(got.value).split(": ", 1)[1]] == ref.value.why
