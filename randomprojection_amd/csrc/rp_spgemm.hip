@@ -2759,9 +2759,25 @@ lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ 
         if (G + cnt > capacity) continue;
         const uint16_t* __restrict__ sc = sp.cols + wt * sp.slot;
         const T* __restrict__ sv = vals + wt * sp.slot;
-        for (uint32_t q = lane; q < cnt; q += 64) {
-            Cj[G + q] = (OI)__builtin_nontemporal_load(sc + q);
-            Cx[G + q] = __builtin_nontemporal_load(sv + q);
+        // kCopyU steps of 64 entries loaded before any is stored (a run is ~6 steps: one round trip)
+        constexpr int kCopyU = 8;
+        for (uint32_t q0 = 0; q0 < cnt; q0 += 64 * kCopyU) {
+            uint16_t cv[kCopyU];
+            T xv[kCopyU];
+#pragma unroll
+            for (int u = 0; u < kCopyU; ++u) {
+                const uint32_t q = q0 + 64 * u + lane;
+                cv[u] = q < cnt ? __builtin_nontemporal_load(sc + q) : (uint16_t)0;
+                xv[u] = q < cnt ? __builtin_nontemporal_load(sv + q) : T(0);
+            }
+#pragma unroll
+            for (int u = 0; u < kCopyU; ++u) {
+                const uint32_t q = q0 + 64 * u + lane;
+                if (q < cnt) {
+                    Cj[G + q] = (OI)cv[u];
+                    Cx[G + q] = xv[u];
+                }
+            }
         }
     }
 }
