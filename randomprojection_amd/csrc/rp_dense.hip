@@ -557,13 +557,110 @@ dense_glds_f64_kernel(const double* __restrict__ A, const double* __restrict__ B
         }
 }
 
+// f64 ring (the default): dense_glds_f64_kernel's tile, fragments and swizzle, but NS = 3 K-tile
+// buffers of 48 KB (144 KB of LDS), so two K-tiles are in flight while one is multiplied (the
+// two-buffer kernel waits vmcnt(0) at the end of every K-tile for the one it issued at the start).
+// The LDS-direct loads are inline asm as in dense_ring_kernel: the compiler then inserts no vmcnt(0)
+// before the fragment reads; the waits below are explicit (6 loads per thread per K-tile).
+__global__ void __launch_bounds__(512)
+dense_ring_f64_kernel(const double* __restrict__ A, const double* __restrict__ B, double* __restrict__ C,
+                      int64_t M, int N, int K, int64_t ldc, unsigned m_tiles, unsigned n_tiles) {
+    constexpr int BM = 256, BN = 128, KC = 8, KT = 16, NS = 3;
+    constexpr int SZ = (BM + BN) * KC;  // uint4 per stage
+    __shared__ uint4 lds[NS * SZ];
+    const unsigned bi = blockIdx.x, xcd = bi & 7u, j = bi >> 3;
+    const unsigned mt = (j / n_tiles) * 8u + xcd, nt = j % n_tiles;
+    if (mt >= m_tiles) return;  // uniform
+    const int64_t m0 = (int64_t)mt * BM;
+    const int n0 = (int)nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 1, wn = w & 1;
+    const int steps = K / KT;
+    const int srow = tid >> 3, sch = tid & 7, sxc = sch ^ (srow & 7);
+    const double* ga[4];
+    const double* gb[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ga[i] = A + std::min<int64_t>(m0 + i * 64 + srow, M - 1) * (int64_t)K + sxc * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) gb[i] = B + (int64_t)std::min(n0 + i * 64 + srow, N - 1) * K + sxc * 2;
+    const uint32_t lds0 = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)reinterpret_cast<uintptr_t>(lds + 64 * w));
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved: the clobber keeps the compiler's own uses safe
+    auto dma = [&](const double* g, uint32_t l) {
+        asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(l) : "memory", "m0");
+    };
+#pragma clang diagnostic pop
+    auto stage = [&](int kt) {
+        const uint32_t base = lds0 + (uint32_t)((kt % NS) * SZ) * 16u;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dma(ga[i] + (int64_t)kt * KT, base + i * 512 * 16);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) dma(gb[i] + (int64_t)kt * KT, base + (BM * KC + i * 512) * 16);
+    };
+    f64x4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int fr = lane & 15, fq = lane >> 4;
+    for (int kt = 0; kt < NS - 1 && kt < steps; ++kt) stage(kt);
+    for (int kt = 0; kt < steps; ++kt) {
+        // K-tile kt landed (this wave's loads; the barrier: everyone's); at most one younger in flight
+        if (kt + 1 < steps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + NS - 1 < steps) stage(kt + NS - 1);  // into the buffer of K-tile kt - 1: all done with it
+        const uint4* sa = lds + (kt % NS) * SZ;
+        const uint4* sb = sa + BM * KC;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int cc = 4 * s + fq;
+            uint4 bfr[4];
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) {
+                const int r = wn * 64 + ni * 16 + fr;
+                bfr[ni] = sb[r * KC + (cc ^ (r & 7))];
+            }
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+                const int r = wm * 64 + mi * 16 + fr;
+                const uint4 afr = sa[r * KC + (cc ^ (r & 7))];
+                const double a0 = __hiloint2double((int)afr.y, (int)afr.x), a1 = __hiloint2double((int)afr.w, (int)afr.z);
+#pragma unroll
+                for (int ni = 0; ni < 4; ++ni) {
+                    const double b0 = __hiloint2double((int)bfr[ni].y, (int)bfr[ni].x);
+                    const double b1 = __hiloint2double((int)bfr[ni].w, (int)bfr[ni].z);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[mi][ni], 0, 0, 0);
+                    acc[mi][ni] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[mi][ni], 0, 0, 0);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+            const int c = n0 + wn * 64 + ni * 16 + fr;
+            if (c >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = m0 + wm * 64 + mi * 16 + fq + 4 * r;
+                if (row < M) C[row * ldc + c] = acc[mi][ni][r];
+            }
+        }
+}
+
 int launch_dense_f64(const void* X, const void* G, double* Y, int64_t n, int64_t m, int64_t p, int64_t ldy,
-                     hipStream_t st) {
+                     hipStream_t st, bool ring) {
     const unsigned m_tiles = (unsigned)((n + 255) / 256), n_tiles = (unsigned)((p + 127) / 128);
     const uint64_t blocks = (uint64_t)((m_tiles + 7) / 8) * 8ull * n_tiles;
     if (blocks >= (1ull << 31)) return fail(RP_ERR_UNSUPPORTED, "too many rows for one launch");
-    hipLaunchKernelGGL(dense_glds_f64_kernel, dim3((unsigned)blocks), dim3(512), 0, st, (const double*)X,
-                       (const double*)G, Y, n, (int)p, (int)m, ldy, m_tiles, n_tiles);
+    if (ring)
+        hipLaunchKernelGGL(dense_ring_f64_kernel, dim3((unsigned)blocks), dim3(512), 0, st, (const double*)X,
+                           (const double*)G, Y, n, (int)p, (int)m, ldy, m_tiles, n_tiles);
+    else
+        hipLaunchKernelGGL(dense_glds_f64_kernel, dim3((unsigned)blocks), dim3(512), 0, st, (const double*)X,
+                           (const double*)G, Y, n, (int)p, (int)m, ldy, m_tiles, n_tiles);
     HIP_TRY(hipGetLastError());
     return RP_OK;
 }
@@ -633,7 +730,7 @@ extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype,
     const int sv = g_dense_variant.load(std::memory_order_relaxed);
     const int v = sv >= 0 ? sv : (dtype == RP_BF16 ? kDenseVariantBf16 : kDenseVariantF32);
     hipStream_t st = (hipStream_t)stream;
-    if (dtype == RP_F64) return launch_dense_f64(X, G, (double*)Y, n, m, p, ldy, st);
+    if (dtype == RP_F64) return launch_dense_f64(X, G, (double*)Y, n, m, p, ldy, st, sv != 10);  // 10: two buffers
     return dtype == RP_BF16 ? dispatch_dense<uint16_t>(v, X, G, (float*)Y, n, m, p, ldy, st)
                             : dispatch_dense<float>(v, X, G, (float*)Y, n, m, p, ldy, st);
 }

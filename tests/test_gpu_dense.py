@@ -61,8 +61,8 @@ def test_mfma_kernel_ragged_shapes(compute, shape, variant):
     from randomprojection_amd import _native as nat
     from randomprojection_amd.gaussian import dense_project_device
 
-    if compute == "fp64" and variant != -1:
-        pytest.skip("one f64 kernel")
+    if compute == "fp64" and variant not in (-1, 10):
+        pytest.skip("two f64 kernels: the ring (default) and the two-buffer one (variant 10)")
     nat.check(nat.load().rp_dense_set_variant(variant))
 
     n, m, p = shape
@@ -80,3 +80,22 @@ def test_mfma_kernel_ragged_shapes(compute, shape, variant):
     dense_project_device(X, C, out=out, compute=compute)
     nat.check(nat.load().rp_dense_set_variant(-1))
     assert np.array_equal(out.cpu().numpy(), Y)
+
+
+@pytest.mark.parametrize("compute", ["bf16", "fp32"])
+def test_side_stream_waits_for_casts(compute):
+    """dense_project_device on a stream other than torch's current one, with operands that need a
+    cast and a K pad (prepared on the current stream): the GEMM waits for them, so the
+    result equals the current-stream run bit for bit."""
+    import torch
+    from randomprojection_amd.gaussian import dense_project_device
+
+    rng = np.random.default_rng(11)
+    X = torch.as_tensor(rng.standard_normal((5000, 4001)), device="cuda")  # f64 in, m not a K-step multiple
+    C = torch.as_tensor(rng.normal(0, 1 / 32, (384, 4001)), device="cuda")
+    want = dense_project_device(X, C, compute=compute)
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    got = dense_project_device(X, C, compute=compute, stream=side.cuda_stream)
+    side.synchronize()
+    assert torch.equal(got, want)
