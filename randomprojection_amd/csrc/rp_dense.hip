@@ -16,6 +16,9 @@
 //    barrier per K-tile (description above the kernel);
 //  * dense_glds_kernel (variant 10): the same tile and staging with two 128-B-per-row buffers, the
 //    next K-tile in flight during this one's MFMAs;
+//  * f64: dense_ring_f64_kernel (the default): 256 x 128 tile, 8 waves of 64 x 64 in
+//    v_mfma_f64_16x16x4_f64, three 48 KB K-tile buffers (two K-tiles in flight); variant 10 selects
+//    the two-buffer dense_glds_f64_kernel (measured 58.7 vs 69.8 TF, profiles/r04_dense_fp64*);
 //  * dense_nt_kernel (variants 0-9; variant 5 = 256 x 256, 8 waves, 32 x 32 MFMAs, two LDS stages, the
 //    round-2 default): the next K step loaded global -> registers during the MFMAs, then written to
 //    the other LDS buffer (one barrier per step); LDS rows of 128 B XOR-swizzled (chunk c of row r at

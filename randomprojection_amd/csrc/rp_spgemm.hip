@@ -9,15 +9,17 @@
 //
 // Pipelines (rp_project_plan reports which one a launch runs):
 //   row-lane (lpr_*, short rows over a packed R, the KDD2012 default): tiles of 256 rows, one wave
-//     per 64 rows, one flat pass per wave builds its rows' output in a fixed LDS slot in
-//     first-touch order (Bloom-flagged rows recomputed exactly), then one scan and one reversing
-//     copy place the slots. R descriptors come either straight from W (direct) or from the staged
-//     gather (count / run-scan / partition / gather kernels: bucket-major segments streamed
-//     against an L2-resident W32 slice); in auto mode lpr_choose_kernel picks one per call on the
-//     device. The staged main kernel is persistent and pipelines the next tile's loads.
+//     per 64-row unit, one flat pass per wave builds its rows' output in a fixed slot in
+//     first-touch order (Bloom-flagged rows recomputed exactly), rows stored in final order; then
+//     one scan and one contiguous copy place the runs. R descriptors come either straight from W
+//     (direct: lpr_main_flat_kernel) or from the staged gather (reserve / partition / gather:
+//     bucket-major segments streamed against an L2-resident W32 slice, then lpr_unsort_kernel puts
+//     the descriptors back in entry order and lpr_wave_kernel runs the flat passes barrier-free);
+//     in auto mode lpr_choose_kernel picks one per call on the device.
 //   tile (spgemm_lookback_kernel, long rows / generic R): one workgroup per tile, products in LDS,
 //     first-touch leaders sum their column groups, decoupled look-back for the tile's offset,
-//     deferred output for tiles whose prefix is late (defer_copy_kernel).
+//     deferred output for tiles whose prefix is late (defer_copy_kernel); opt-in filtered form
+//     (RP_OPT_FILTER: filter_* kernels drop the A entries whose R row is empty first).
 // Tiles past the LDS caps in either pipeline run scipy's dense sums/next accumulator exactly
 // (heavy_tile), so any input is handled.
 #include <hip/hip_runtime.h>
@@ -1281,11 +1283,11 @@ filter_write_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, c
 }
 
 // ------------------------------------------------------------------------------------------
-// Row-lane pipeline (DESIGN.md §3c; packed R, short rows — KDD2012: 11 entries, 6 products/row).
+// Row-lane pipeline (DESIGN.md §3.1; packed R, short rows — KDD2012: 11 entries, 6 products/row).
 // No look-back and no waiting: every wave's output goes to a fixed slot, then one scan and one copy.
 //   lpr_main_kernel   one workgroup per tile of 256 rows, one wave per 64 rows. The tile's R
 //                     descriptors (gathered from W directly, or the staged W32 words of
-//                     stage_partition/stage_gather) land in LDS by entry; then each wave runs ONE
+//                     lpr_partition/lpr_gather) land in LDS by entry; then each wave runs ONE
 //                     flat pass over its entries (64 consecutive entries per step, no divergence):
 //                     row of an entry from a row-start bitmap (popcount), its products, their kept
 //                     prefix (wave scan) = their place in the wave's slot in first-touch order, and
