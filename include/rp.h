@@ -20,11 +20,13 @@
  *                                                        code/clustermode/randomProjection.py:46
  *      -> scipy _sparsetools.csr_matmat_maxnnz + csr_matmat  scipy/sparse/_compressed.py:569-595
  *    Device-resident CSR in, device-resident CSR out, asynchronous on one stream. The call runs one
- *    of two kernel pipelines (rp_project_plan): the row-lane pipeline for short rows over a packed
- *    R (KDD2012: staging choice, segment reserves, super-tile partition, filtered gather, unsort,
- *    wave kernel (or the direct main kernel when the device picks direct gathers), heavy-tile
- *    count/write, scan, copy) or the tile pipeline for long rows / generic R (one look-back kernel
- *    + a copy of deferred tiles). Output equals scipy's bit for bit: same per-row order
+ *    of the kernel pipelines rp_project_plan reports: the row-lane pipeline for short rows over a
+ *    packed R (KDD2012: staging choice, segment reserves, super-tile partition, filtered gather,
+ *    unsort, wave kernel (or the direct main kernel when the device picks direct gathers),
+ *    heavy-tile count/write, scan, copy), the tile pipeline for long rows / generic R (one
+ *    look-back kernel + a copy of deferred tiles), or, opt-in (RP_OPT_FILTER), the tile pipeline
+ *    behind passes that drop the A entries whose R row is empty (one host sync per call for its
+ *    row chunks). Output equals scipy's bit for bit: same per-row order
  *    (RP_ORDER_SCIPY = reverse first-touch) or ascending (RP_ORDER_SORTED = what pyspark's
  *    SparseVector makes of it, code/clustermode/randomProjection.py:49-50), same zero drop, values
  *    computed with the same separately rounded multiply and add.
