@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--ring", type=int, default=3)
     ap.add_argument("--no-stream", action="store_true")
     ap.add_argument("--variant", type=int, default=-1, help="librp dense tile variant (rp_dense_set_variant)")
+    ap.add_argument("--lib", default=None, help="another librp build (A/B measurements; its id is reported)")
     args = ap.parse_args()
 
     import torch
@@ -48,7 +49,7 @@ def main():
 
     from randomprojection_amd import _native as nat
 
-    nat.check(nat.load().rp_dense_set_variant(args.variant))
+    nat.check(nat.load(args.lib).rp_dense_set_variant(args.variant))
     torch.cuda.set_device(0)
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[args.compute]
     C = torch.as_tensor(gaussian_random_matrix(args.p, args.m, random_state=123).astype("float32"), device="cuda")
