@@ -1320,6 +1320,31 @@ struct LprSpace {
 
 __device__ __forceinline__ uint32_t lpr_h2(uint32_t col) { return (col * 0x9E3779B1u) >> 26; }
 
+// Bloom check of one row's slot range [kst, kst + n): 3 x 64-bit filters in registers; true if a
+// column finds its three bits already set by an earlier one (every real repeat does; false alarms
+// ~ (i/64)^3 for the i-th product). Columns are read four at a time (four LDS loads in flight per
+// round trip instead of one); a row without slot entries (n = 0) checks nothing.
+__device__ __forceinline__ bool lpr_bloom(const uint16_t* cb, uint32_t kst, uint32_t n) {
+    uint64_t b0 = 0, b1 = 0, b2 = 0;
+    bool hit = false;
+    for (uint32_t q0 = 0; q0 < n; q0 += 4) {
+        uint32_t c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = q0 + u < n ? (uint32_t)cb[kst + q0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (q0 + u < n) {
+                const uint32_t col = c[u];
+                const uint64_t m0 = 1ull << (col & 63), m1 = 1ull << ((col >> 6) & 63), m2 = 1ull << lpr_h2(col);
+                hit |= (b0 & m0) && (b1 & m1) && (b2 & m2);
+                b0 |= m0;
+                b1 |= m1;
+                b2 |= m2;
+            }
+    }
+    return hit;
+}
+
 // A wave's rows to HBM in their final order, back to back (row r's kept entries [kst, kst + kept)
 // of the LDS slot, reversed for scipy's reverse first-touch order or as built for RP_ORDER_SORTED;
 // gaps the exact path left between rows are squeezed out), so that the copy kernel moves one
@@ -1762,17 +1787,7 @@ lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             const uint32_t kend_r = nx < 64 ? kst_next : carry_k;
             uint32_t kept = nonempty ? kend_r - kst : 0u;
             bool hit = false;
-            if (!overflow) {
-                uint64_t b0 = 0, b1 = 0, b2 = 0;
-                for (uint32_t q = kst; q < kend_r; ++q) {
-                    const uint32_t col = cb[q];
-                    const uint64_t m0 = 1ull << (col & 63), m1 = 1ull << ((col >> 6) & 63), m2 = 1ull << lpr_h2(col);
-                    hit |= (b0 & m0) && (b1 & m1) && (b2 & m2);
-                    b0 |= m0;
-                    b1 |= m1;
-                    b2 |= m2;
-                }
-            }
+            if (!overflow) hit = lpr_bloom(cb, kst, kept);
             uint64_t todo = s_susp[w] | __ballot(hit);  // lane == row within the wave
             __builtin_amdgcn_wave_barrier();  // the row-start bitmap is dead from here: the scratch reuses it
             constexpr int kScr = (int)((kLprFlagWords * 8 - 16) / (2 + sizeof(T)));
@@ -2178,17 +2193,7 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     const uint32_t kend = nxt < 64 ? kst_next : carry_k;
     uint32_t kept = nonempty ? kend - kst : 0u;
     bool hit = false;
-    if (!overflow) {
-        uint64_t b0 = 0, b1 = 0, b2 = 0;
-        for (uint32_t q = kst; q < kend; ++q) {
-            const uint32_t col = cb[q];
-            const uint64_t m0 = 1ull << (col & 63), m1 = 1ull << ((col >> 6) & 63), m2 = 1ull << lpr_h2(col);
-            hit |= (b0 & m0) && (b1 & m1) && (b2 & m2);
-            b0 |= m0;
-            b1 |= m1;
-            b2 |= m2;
-        }
-    }
+    if (!overflow) hit = lpr_bloom(cb, kst, kept);
     uint64_t todo = s_susp[w] | __ballot(hit);  // lane == row within the wave
     __builtin_amdgcn_wave_barrier();  // the row-start bitmap is dead from here: the scratch reuses it
     constexpr int kScr = (int)((kLprFlagWords * 8 - 16) / (2 + sizeof(T)));
@@ -2556,17 +2561,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     const uint32_t kend_r = nx < 64 ? kst_next : carry_k;
     uint32_t kept = nonempty ? kend_r - kst : 0u;
     bool hit = false;
-    if (!overflow) {
-        uint64_t b0 = 0, b1 = 0, b2 = 0;
-        for (uint32_t q = kst; q < kend_r; ++q) {
-            const uint32_t col = cb[q];
-            const uint64_t m0 = 1ull << (col & 63), m1 = 1ull << ((col >> 6) & 63), m2 = 1ull << lpr_h2(col);
-            hit |= (b0 & m0) && (b1 & m1) && (b2 & m2);
-            b0 |= m0;
-            b1 |= m1;
-            b2 |= m2;
-        }
-    }
+    if (!overflow) hit = lpr_bloom(cb, kst, kept);
     uint64_t todo = s_susp | __ballot(hit);  // lane == row within the unit
     if (__ballot(overflow)) todo = 0;
     // exact path, one flagged row at a time, the whole wave on it: its products in sequence order
