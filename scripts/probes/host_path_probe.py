@@ -1,4 +1,6 @@
-"""Where does the host CSR -> host CSR call (boundary 2) spend its time? Components timed separately."""
+"""(Historical, round 1: it sets environment knobs librp no longer reads — rp_projector_set_option
+replaced them in round 3; kept as the record of DESIGN.md §3d's measurement.)
+Where does the host CSR -> host CSR call (boundary 2) spend its time? Components timed separately."""
 import json, os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

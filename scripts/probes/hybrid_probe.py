@@ -1,4 +1,6 @@
-"""Feasibility probe for a hybrid direct + staged step (configs[1] shape), measurement only.
+"""(Historical, round 1: it sets environment knobs librp no longer reads — rp_projector_set_option
+replaced them in round 3; kept as the record of DESIGN.md §3d's measurement.)
+Feasibility probe for a hybrid direct + staged step (configs[1] shape), measurement only.
 
 (1) Direct tile kernel alone with fewer tiles resident per CU (RP_DEBUG_LDS_PAD inflates its LDS):
     does the random-line request rate still saturate with a fraction of the slots?
