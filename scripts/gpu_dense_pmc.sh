@@ -6,9 +6,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-for c in bf16 fp32; do
+for c in ${COMPUTES:-bf16 fp32 fp64}; do
   i=0
-  for pmc in "MfmaUtil" "MfmaFlopsBF16 MfmaFlopsF32"; do
+  for pmc in "MfmaUtil" "MfmaFlopsBF16 MfmaFlopsF32 MfmaFlopsF64"; do
     i=$((i+1))
     timeout -s KILL 240 rocprofv3 --pmc $pmc -T --output-format csv -d gpurun_out/dense_pmc_${c}_$i -o pmc -- python3 scripts/bench_dense.py --compute $c --steps 3 --warmup 1 --no-stream > gpurun_out/dense_pmc_${c}_$i.log 2>&1 || { tail -20 gpurun_out/dense_pmc_${c}_$i.log; exit 6; }
   done
