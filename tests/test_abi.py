@@ -71,3 +71,18 @@ def test_touched_source_is_a_stale_library(tmp_path):
         assert "rebuild" in str(e)
     else:
         raise AssertionError("a touched source was not detected")
+
+
+def test_committed_traffic_matches_sources():
+    """profiles/traffic_latest.json (the PMC HBM bytes bench.py puts in roofline.traffic) was
+    measured on the library built from the sources on disk: bench.py only uses it when its
+    src_sha16 equals the loaded build id, so a source change without a re-profile shows up here
+    rather than as a silent traffic=null in the round-end bench line."""
+    import json
+
+    from randomprojection_amd import build
+
+    with open(os.path.join(ROOT, "profiles", "traffic_latest.json")) as f:
+        tj = json.load(f)
+    assert tj["src_sha16"] == build.source_id()
+    assert tj["hbm_bytes_per_launch"] > 0
