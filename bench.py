@@ -101,21 +101,16 @@ def launch_ranks(n: int) -> int:
 
 
 def step_kernels(plan, staged_run):
-    """The kernels one rp_project_device call runs for this plan (rp_spgemm.hip); in auto mode the
-    other branch's kernels are launched too and exit at once."""
+    """The kernels one rp_project_device call runs for this plan (rp_spgemm.hip). In auto mode the
+    host reads lpr_choose_kernel's verdict and launches only the chosen branch."""
     if plan["pipeline"] == "rowlane":
-        main = (["lpr_unsort_kernel", "lpr_wave_kernel"] if plan.get("split", True) else ["lpr_main_kernel"])
-        ks = (main if staged_run else ["lpr_main_flat_kernel"]) + ["lpr_heavy_count_kernel",
-                                                                  "lpr_scan_kernel", "lpr_copy_kernel",
-                                                                  "lpr_heavy_write_kernel"]
-        if staged_run:
-            ks = ["lpr_reserve_kernel", "lpr_partition_kernel",
-                  "lpr_gather_kernel"] + ks
+        main = ["lpr_reserve_kernel", "lpr_partition_kernel", "lpr_gather_kernel",
+                "lpr_wave_kernel"] if staged_run else ["lpr_main_flat_kernel"]
+        ks = main + ["lpr_heavy_count_kernel", "lpr_scan_kernel", "lpr_copy_kernel", "lpr_heavy_write_kernel"]
         if plan["staged"] == "auto":
             ks = ["lpr_choose_kernel"] + ks
         return ks
-    ks = ["spgemm_lookback_kernel", "defer_copy_kernel"]
-    return (["filter_probe_kernel", "filter_kernel"] + ks) if plan["pipeline"] == "tile_filtered" else ks
+    return ["spgemm_lookback_kernel", "defer_copy_kernel"]
 
 
 def algorithmic_bytes_per_row(a, rbar, c):
@@ -145,10 +140,6 @@ def main():
     ap.add_argument("--stage-shift", type=int, default=0, help="2^shift features per staging bucket (0 = auto)")
     ap.add_argument("--pipeline", choices=["auto", "tile", "rowlane"], default="auto",
                     help="force a kernel pipeline where it can run (results identical; measurements)")
-    ap.add_argument("--filter", type=int, choices=[-1, 0, 1], default=-1,
-                    help="tile pipeline: drop A entries with empty R rows first (-1 auto, 0 off, 1 on)")
-    ap.add_argument("--lpr-split", type=int, choices=[-1, 0, 1], default=-1,
-                    help="staged row-lane: 1 unsort + wave kernels (default), 0 the persistent main kernel")
     ap.add_argument("--cpu-sample-rows", type=int, default=None)
     ap.add_argument("--cpu-part-rows", type=int, default=100_000,
                     help="rows per recipe partition (one per core) in the CPU baseline")
@@ -286,8 +277,6 @@ def main():
         P.set_staging(args.staging, args.stage_shift)
     if args.pipeline != "auto":
         P.set_option("pipeline", args.pipeline)
-    P.set_option("lpr_split", args.lpr_split)
-    P.set_option("filter", args.filter)
     try:  # full workspace (deferred tile output + staging); the minimal one if HBM is short
         ws = torch.empty(P.workspace_bytes(args.rows, nnz_a, dtype=Ax.dtype), dtype=torch.uint8, device=dev)
     except torch.OutOfMemoryError:

@@ -19,14 +19,13 @@
  *      projected_features = features_matrix.dot(local_csr_matrix)
  *                                                        code/clustermode/randomProjection.py:46
  *      -> scipy _sparsetools.csr_matmat_maxnnz + csr_matmat  scipy/sparse/_compressed.py:569-595
- *    Device-resident CSR in, device-resident CSR out, asynchronous on one stream. The call runs one
- *    of the kernel pipelines rp_project_plan reports: the row-lane pipeline for short rows over a
- *    packed R (KDD2012: staging choice, segment reserves, super-tile partition, filtered gather,
- *    unsort, wave kernel (or the direct main kernel when the device picks direct gathers),
- *    heavy-tile count/write, scan, copy), the tile pipeline for long rows / generic R (one
- *    look-back kernel + a copy of deferred tiles), or, opt-in (RP_OPT_FILTER), the tile pipeline
- *    behind passes that drop the A entries whose R row is empty (one host sync per call for its
- *    row chunks). Output equals scipy's bit for bit: same per-row order
+ *    Device-resident CSR in, device-resident CSR out, asynchronous on one stream (in auto staging
+ *    mode the host reads a 4-byte verdict of a sampling kernel first). The call runs one of the
+ *    kernel pipelines rp_project_plan reports: the row-lane pipeline for short rows over a packed R
+ *    (KDD2012: staging choice, then either segment reserves, super-tile partition, bitmap-filtered
+ *    gather and the wave kernel, or the direct main kernel; heavy-tile count/write, scan, copy), or
+ *    the tile pipeline for long rows / generic R (one look-back kernel + a copy of deferred tiles).
+ *    Output equals scipy's bit for bit: same per-row order
  *    (RP_ORDER_SCIPY = reverse first-touch) or ascending (RP_ORDER_SORTED = what pyspark's
  *    SparseVector makes of it, code/clustermode/randomProjection.py:49-50), same zero drop, values
  *    computed with the same separately rounded multiply and add.
@@ -178,42 +177,35 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
  *   RP_OPT_DEFER_TICKS   256-row tiles' look-back wait budget in s_memrealtime ticks (100 MHz):
  *                        -1 default (800 = 8 us); n >= 0 override
  *   RP_OPT_CHUNK_ROWS    row-lane rows per launch sequence: 0 default (2^27), else rounded up to
- *                        whole 256-row tiles; also caps the filtered tile pipeline's rows per chunk
- *                        (a cap below n_rows / 4096 makes that call run unfiltered)
+ *                        whole 256-row tiles
  *   RP_OPT_HOST_THREADS  helper threads of the host result download: -1 default (min(4, cores));
  *                        0 or 1 plain copies
- *   RP_OPT_LPR_SPLIT     staged row-lane pipeline: -1 default (split), 1 split = unsort kernel +
- *                        barrier-free wave kernel, 0 the persistent main kernel
- *   RP_OPT_FILTER        tile pipeline over a packed R (m <= 2^26): 1 on — streaming passes first drop
- *                        the A entries whose R row is empty (row chunks of <= 2^30 entries); -1 auto
- *                        and 0 off (the default: measured slower on configs[3]) */
+ * (Options 6 and 7 — the persistent row-lane kernel and the filtered tile pipeline, both measured
+ * slower than the defaults — were removed in round 5 and are rejected as unknown.) */
 typedef enum {
     RP_OPT_PIPELINE = 1,
     RP_OPT_DEFER_POLLS = 2,
     RP_OPT_DEFER_TICKS = 3,
     RP_OPT_CHUNK_ROWS = 4,
-    RP_OPT_HOST_THREADS = 5,
-    RP_OPT_LPR_SPLIT = 6,
-    RP_OPT_FILTER = 7
+    RP_OPT_HOST_THREADS = 5
 } rp_option;
 int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value);
 int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* value);
 
 /* The kernel pipeline rp_project_device would run for n_rows rows holding nnz_a entries with the
- * full workspace: *pipeline = RP_PIPE_TILE (one-launch tile SpGEMM with look-back),
- * RP_PIPE_ROWLANE (row-lane kernel: short rows over a packed R) or RP_PIPE_TILE_FILTERED (the tile
- * SpGEMM on A without its entries whose R row is empty, RP_OPT_FILTER), *staged = 1 if the R descriptors
+ * full workspace: *pipeline = RP_PIPE_TILE (one-launch tile SpGEMM with look-back) or
+ * RP_PIPE_ROWLANE (row-lane kernel: short rows over a packed R), *staged = 1 if the R descriptors
  * are fetched by the staged gather, 0 if gathered directly, 2 if the device decides per call (auto
  * mode, rp_project_choice), *bucket_shift the staged bucket width (log2 features). Any out
  * pointer may be NULL. For logging and benchmarks; results are identical on every pipeline. */
-typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1, RP_PIPE_TILE_FILTERED = 2 } rp_pipeline;
+typedef enum { RP_PIPE_TILE = 0, RP_PIPE_ROWLANE = 1 } rp_pipeline;
 int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_t* pipeline, int32_t* staged,
                     int32_t* bucket_shift);
 
 /* After an rp_project_device call with `workspace` has completed (its stream synchronised by the
  * caller): *staged = 1 if that call used the staged gather, 0 if direct gathers (rp_project_plan's
- * *staged == 2: decided on the device per call, from a sample of the input's feature ids; and a
- * staged row-lane call whose columns overflowed a segment's reserve finishes direct and reads 0).
+ * *staged == 2: decided per call from a sample of the input's feature ids taken on the device; and
+ * a staged row-lane call whose columns overflowed a segment's reserve finishes direct and reads 0).
  * The call records what actually ran in the workspace header, so a re-planned call (a workspace
  * too small for staging) reads 0. n_rows / nnz_a are unused (kept for the ABI). 4-byte copy. */
 int rp_project_choice(const rp_projector* h, int64_t n_rows, int64_t nnz_a, const void* workspace,
@@ -313,11 +305,10 @@ int rp_synth_libsvm_device(int device, int64_t n_rows, const int64_t* indptr, co
  * MFMA products, f32 accumulate, Y f32) or RP_F64 (f64 MFMA, Y f64), both row-major, 16-byte aligned,
  * m a multiple of 64 (bf16) / 32 (f32) / 16 (f64). Replaces sklearn GaussianRandomProjection.transform's
  * X @ components_.T (sklearn/random_projection.py:569-612), computed in X's dtype as sklearn does,
- * with hand-written MFMA GEMMs. Asynchronous on `stream`. */
+ * with hand-written MFMA GEMMs. Asynchronous on `stream`. variant: -1 = the default kernel; 0..11 pick
+ * another measured tile variant for this call only (A/B measurements; rp_dense.hip lists them). */
 int rp_dense_project_device(int device, const void* X, int32_t dtype, int64_t n, int64_t m, const void* G,
-                            int64_t p, void* Y, int64_t ldy, void* stream);
-/* Library-wide tile variant of rp_dense_project_device (measurements): -1 = the default. */
-int rp_dense_set_variant(int32_t variant);
+                            int64_t p, void* Y, int64_t ldy, void* stream, int32_t variant);
 
 #ifdef __cplusplus
 }

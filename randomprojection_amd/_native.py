@@ -15,8 +15,6 @@ RP_I32, RP_I64, RP_F32, RP_F64, RP_BF16 = 1, 2, 3, 4, 5
 RP_LAYOUT_AUTO, RP_LAYOUT_GENERIC, RP_LAYOUT_PACKED = 0, 1, 2
 RP_ORDER_SCIPY, RP_ORDER_SORTED = 0, 1
 RP_OPT_PIPELINE, RP_OPT_DEFER_POLLS, RP_OPT_DEFER_TICKS, RP_OPT_CHUNK_ROWS, RP_OPT_HOST_THREADS = 1, 2, 3, 4, 5
-RP_OPT_LPR_SPLIT = 6
-RP_OPT_FILTER = 7
 
 # every symbol include/rp.h declares (tests/test_abi.py checks the .so exports them all)
 EXPORTS = (
@@ -27,7 +25,7 @@ EXPORTS = (
     "rp_projector_set_option", "rp_projector_get_option", "rp_project_device",
     "rp_project_host_begin", "rp_result_fetch", "rp_result_free", "rp_project",
     "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_libsvm_project_stream", "rp_synth_libsvm_device", "rp_project_stream", "rp_host_alloc", "rp_host_free",
-    "rp_dense_project_device", "rp_dense_set_variant",
+    "rp_dense_project_device",
 )
 
 
@@ -162,8 +160,7 @@ def load(path: str = None, verify: bool = None):
         "rp_host_free": (ctypes.c_int, [vp]),
         "rp_synth_rows_device": (ctypes.c_int, [ctypes.c_int, i64, i64, dbl, i32, i32, dbl, ctypes.c_uint64,
                                                 vp, i32, vp, vp, vp, P(i64)]),
-        "rp_dense_project_device": (ctypes.c_int, [ctypes.c_int, vp, i32, i64, i64, vp, i64, vp, i64, vp]),
-        "rp_dense_set_variant": (ctypes.c_int, [i32]),
+        "rp_dense_project_device": (ctypes.c_int, [ctypes.c_int, vp, i32, i64, i64, vp, i64, vp, i64, vp, i32]),
         "rp_libsvm_parse_device": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, vp, vp, i32, vp, vp, i64, i64, vp,
                                                   P(i64), P(i64), P(i64)]),
         "rp_libsvm_project_stream": (ctypes.c_int, [vp, vp, i64, i32, i64, vp, i64, P(CsrOut), P(i64), P(i64),

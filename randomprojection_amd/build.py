@@ -29,16 +29,20 @@ FLAGS = [
     "-ffp-contract=off", "-fno-fast-math", "-Wall",
 ]
 MARKER = b"rp-src-sha16:"
+HASHED = DEPS + ["randomprojection_amd/build.py"]  # files source_id covers (plus HIPCC and FLAGS)
 
 
 def source_id(root: str = ROOT) -> str:
-    """sha256 prefix over (path, contents) of every source file of librp under ``root``."""
+    """sha256 prefix over (path, contents) of every source file of librp under ``root``, plus the
+    compiler path and flags and this build script (a changed flag such as -ffp-contract, which the
+    bit-exactness depends on, must rebuild and must make the loader refuse the old binary)."""
     h = hashlib.sha256()
-    for rel in DEPS:
+    for rel in HASHED:
         h.update(rel.encode() + b"\0")
         with open(os.path.join(root, rel), "rb") as f:
             h.update(f.read())
         h.update(b"\0")
+    h.update(("\0".join([HIPCC, *FLAGS])).encode())
     return h.hexdigest()[:16]
 
 
@@ -57,27 +61,22 @@ def needs_build(out: str = OUT) -> bool:
     return library_id(out) != source_id()
 
 
-DIAG_OUT = os.path.join(HERE, "librp_diag.so")
-
-
-def build(force: bool = False, verbose: bool = False, diag: bool = False) -> str:
-    """librp.so; ``diag=True`` builds librp_diag.so instead (in-kernel stage stamps, -DRP_STAMPS),
-    used only by scripts/stage_stamps.py, never by the package. Sources compile in parallel (one
-    hipcc per .hip into build/), then link."""
-    out = DIAG_OUT if diag else OUT
+def build(force: bool = False, verbose: bool = False) -> str:
+    """librp.so. Sources compile in parallel (one hipcc per .hip into build/), then link."""
+    out = OUT
     os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
     # one build at a time (two importers racing on the same objects); re-check under the lock
     with open(os.path.join(HERE, "build", ".lock"), "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
         if force or needs_build(out):
-            _compile_and_link(out, diag, verbose)
+            _compile_and_link(out, verbose)
     return out
 
 
-def _compile_and_link(out: str, diag: bool, verbose: bool) -> None:
+def _compile_and_link(out: str, verbose: bool) -> None:
     sid = source_id()
-    extra = [f'-DRP_SRC_SHA16="{sid}"'] + (["-DRP_STAMPS"] if diag else [])
-    odir = os.path.join(HERE, "build", "diag" if diag else "rel")
+    extra = [f'-DRP_SRC_SHA16="{sid}"']
+    odir = os.path.join(HERE, "build", "rel")
     os.makedirs(odir, exist_ok=True)
     objs, procs = [], []
     for src in SRC:
@@ -100,4 +99,4 @@ def _compile_and_link(out: str, diag: bool, verbose: bool) -> None:
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True, diag="--diag" in sys.argv))
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -9,7 +9,7 @@
 //   bf16: bf16 operands, f32 accumulate, f32 result (v_mfma_f32_16x16x32_bf16 / _32x32x16_bf16).
 //   f32:  exact f32 products (gfx950 has no xf32), f32 accumulate (v_mfma_f32_16x16x4_f32 / _32x32x2_f32).
 //
-// Kernel families (rp_dense_set_variant picks one for measurements):
+// Kernel families (rp_dense_project_device's `variant` picks one for measurements):
 //  * dense_ring_kernel (variant 11, the default): 256 x 256 tile, 8 waves of 128 x 64, 16 x 16
 //    MFMAs, operands staged global -> LDS by global_load_lds_dwordx4 (no VGPR round trip) into a
 //    ring of four 64-B-per-row K-tile buffers, three K-tiles in flight while one is multiplied, one
@@ -681,7 +681,7 @@ int launch_dense(const void* X, const void* G, float* Y, int64_t n, int64_t m, i
     return RP_OK;
 }
 
-// tile variants (RP_DENSE_VARIANT, measurements): 0 = 128x128 2 stages, 1 = 128x128 1 stage,
+// tile variants (the `variant` argument, measurements): 0 = 128x128 2 stages, 1 = 128x128 1 stage,
 // 2 = 256x128 1 stage, 3 = 128x256 2 stages (8 waves), 4 = 256x256 1 stage (8 waves), 5 = 256x256
 // 2 stages (128 KB LDS, 8 waves)
 // defaults: the four-stage LDS-direct ring for both (measured, profiles/r03_dense_*: bf16 1114 TF vs
@@ -707,19 +707,13 @@ int dispatch_dense(int v, const void* X, const void* G, float* Y, int64_t n, int
     }
 }
 
-std::atomic<int> g_dense_variant{-1};  // rp_dense_set_variant (measurements); -1 = kDenseVariant
-
 }  // namespace
 
-extern "C" int rp_dense_set_variant(int32_t variant) {
-    if (variant < -1 || variant > 11) return fail(RP_ERR_INVALID, "variant must be -1 (default) or 0..11");
-    g_dense_variant.store(variant, std::memory_order_relaxed);
-    return RP_OK;
-}
-
 extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype, int64_t n, int64_t m,
-                                       const void* G, int64_t p, void* Y, int64_t ldy, void* stream) {
+                                       const void* G, int64_t p, void* Y, int64_t ldy, void* stream,
+                                       int32_t variant) {
     if (!X || !G || !Y) return fail(RP_ERR_INVALID, "NULL operand");
+    if (variant < -1 || variant > 11) return fail(RP_ERR_INVALID, "variant must be -1 (default) or 0..11");
     if (dtype != RP_F32 && dtype != RP_BF16 && dtype != RP_F64)
         return fail(RP_ERR_INVALID, "dtype must be RP_F32, RP_BF16 or RP_F64");
     if (n < 0 || m <= 0 || p <= 0 || ldy < p) return fail(RP_ERR_INVALID, "bad shape");
@@ -730,7 +724,7 @@ extern "C" int rp_dense_project_device(int device, const void* X, int32_t dtype,
     if (al & 15) return fail(RP_ERR_INVALID, "X and G must be 16-byte aligned");
     if (n == 0) return RP_OK;
     HIP_TRY(hipSetDevice(device));
-    const int sv = g_dense_variant.load(std::memory_order_relaxed);
+    const int sv = variant;  // per call (measurements); -1 = the default
     const int v = sv >= 0 ? sv : (dtype == RP_BF16 ? kDenseVariantBf16 : kDenseVariantF32);
     hipStream_t st = (hipStream_t)stream;
     if (dtype == RP_F64) return launch_dense_f64(X, G, (double*)Y, n, m, p, ldy, st, sv != 10);  // 10: two buffers

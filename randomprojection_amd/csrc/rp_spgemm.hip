@@ -11,15 +11,14 @@
 //   row-lane (lpr_*, short rows over a packed R, the KDD2012 default): tiles of 256 rows, one wave
 //     per 64-row unit, one flat pass per wave builds its rows' output in a fixed slot in
 //     first-touch order (Bloom-flagged rows recomputed exactly), rows stored in final order; then
-//     one scan and one contiguous copy place the runs. R descriptors come either straight from W
+//     one scan and one contiguous copy place the runs. R descriptors come either straight from W32
 //     (direct: lpr_main_flat_kernel) or from the staged gather (reserve / partition / gather:
-//     bucket-major segments streamed against an L2-resident W32 slice, then lpr_unsort_kernel puts
-//     the descriptors back in entry order and lpr_wave_kernel runs the flat passes barrier-free);
-//     in auto mode lpr_choose_kernel picks one per call on the device.
+//     bucket-major segments streamed against an L2-resident W32 slice; lpr_wave_kernel reads its
+//     unit's parts of the runs and puts the descriptors back in entry order in LDS); in auto mode
+//     lpr_choose_kernel samples the feature ids and the host launches the chosen branch only.
 //   tile (spgemm_lookback_kernel, long rows / generic R): one workgroup per tile, products in LDS,
 //     first-touch leaders sum their column groups, decoupled look-back for the tile's offset,
-//     deferred output for tiles whose prefix is late (defer_copy_kernel); opt-in filtered form
-//     (RP_OPT_FILTER: filter_* kernels drop the A entries whose R row is empty first).
+//     deferred output for tiles whose prefix is late (defer_copy_kernel).
 // Tiles past the LDS caps in either pipeline run scipy's dense sums/next accumulator exactly
 // (heavy_tile), so any input is handled.
 #include <hip/hip_runtime.h>
@@ -58,21 +57,6 @@ constexpr uint64_t kFlagA = 1ull << 62;   // tile aggregate published
 constexpr uint64_t kFlagP = 2ull << 62;   // tile inclusive prefix published
 constexpr uint64_t kValMask = (1ull << 62) - 1;
 constexpr long kSpinLimit = 1l << 27;     // bounded waits (with s_sleep): seconds, never minutes
-
-// Diagnostic builds (-DRP_STAMPS, librp_diag.so only): thread 0 of each tile records
-// s_memrealtime (100 MHz) at stage boundaries into g_stamps[tile * 8 + k]. Never in librp.so.
-#ifdef RP_STAMPS
-__device__ unsigned long long* g_stamps;
-#define STAMP(k)                                                                                  \
-    do {                                                                                          \
-        if (threadIdx.x == 0 && g_stamps)                                                         \
-            g_stamps[(size_t)tile * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
-    } while (0)
-#else
-#define STAMP(k) \
-    do {         \
-    } while (0)
-#endif
 
 struct Workspace {              // device memory header; tile states follow at +64 bytes
     unsigned int tile_counter;
@@ -114,9 +98,10 @@ struct DeferSpace {
 struct PackedR {
     const uint64_t* W;
     const uint16_t* O;
+    const uint64_t* SW;  // side table: W words of the features with > 2 entries (W32 code 3), or NULL
 };
 constexpr uint64_t kOvf = 7ull << 61;
-constexpr uint32_t kW32J = (1u << 26) - 1;  // feature index bits of a code-3 W32 word (m <= 2^26)
+constexpr uint32_t kW32J = (1u << 26) - 1;  // side-table index bits of a code-3 W32 word (m <= 2^26)
 constexpr uint64_t kLow61 = (1ull << 61) - 1;
 // Generic CSR (any values): Bp int32 (m + 1), Bj uint16, Bx in the compute type.
 template <typename T>
@@ -238,18 +223,16 @@ __device__ unsigned long long wave_sum_u64(unsigned long long v) {
 
 // max_polls < 0: wait (bounded by kSpinLimit); otherwise give up after max_polls unsuccessful
 // polls, return ~0ull and leave only the aggregate published. publish_agg = false: the aggregate
-// is already there (defer_copy_kernel). base0 (tile 0's prefix): the entries of earlier row chunks
-// of the same call (filtered tile pipeline), read by tile 0 only; null = 0.
+// is already there (defer_copy_kernel).
 __device__ unsigned long long lookback_wave(unsigned long long* states, unsigned int tile,
                                             unsigned long long agg, Workspace* ws,
                                             long max_polls = -1, bool publish_agg = true,
-                                            long max_ticks = 0, const unsigned long long* base0 = nullptr) {
+                                            long max_ticks = 0) {
     const int lane = threadIdx.x & 63;
     if (tile == 0) {
-        const unsigned long long b = base0 ? *base0 : 0ull;
         if (lane == 0)
-            __hip_atomic_store(&states[0], kFlagP | (b + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return b;
+            __hip_atomic_store(&states[0], kFlagP | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0ull;
     }
     if (lane == 0 && publish_agg)
         __hip_atomic_store(&states[tile], kFlagA | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -472,8 +455,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
                        OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
                        unsigned long long capacity, Caps caps, int order, Workspace* ws,
-                       unsigned int n_tiles, DeferSpace dfr, int defer_polls, int defer_ticks,
-                       const unsigned long long* __restrict__ cbase) {
+                       unsigned int n_tiles, DeferSpace dfr, int defer_polls, int defer_ticks) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ uint16_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative, <= cap_a)
     __shared__ uint16_t s_rowS[kBlock + 1];    // row -> first product
@@ -492,7 +474,6 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
     __syncthreads();
     const unsigned int tile = s_tile;
     if (tile >= n_tiles) return;  // uniform
-    STAMP(0);
 
     const int64_t row0 = (int64_t)tile * caps.rpt;
     const int nrows = (int)std::min<int64_t>(caps.rpt, n_rows - row0);
@@ -529,7 +510,6 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
             }
         }
         __syncthreads();
-        STAMP(1);
         // ---- stage 1b: product offsets per entry; entry -> row map; row product ranges
         if (tid < nrows)
             for (uint32_t e = s_rowptr[tid]; e < s_rowptr[tid + 1]; ++e) s_erow[e] = (uint8_t)tid;
@@ -541,7 +521,6 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                 s_rowS[r] = (uint16_t)rs;
                 if (r < nrows && s_eoff[s_rowptr[r + 1]] - rs > (uint32_t)kRowProdMax) s_heavy = 1;
             }
-        STAMP(2);
         if (fits) {
             // ---- stage 1c: every product x*b (one rounding), grouped by row, in (jj, kk) order
 #pragma unroll
@@ -565,7 +544,6 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
             if (tid < 4 && P_t + tid < (uint32_t)caps.cap_p && ((P_t + tid) >> 2) == (P_t >> 2))
                 s_pkr[P_t + tid] = 0xffffffffu;
             __syncthreads();
-            STAMP(3);
             if (!s_heavy) {  // uniform
                 // ---- stage 2: flat over products. A product leads its column group if no earlier
                 // product of its row has that column (= scipy's first touch); the leader sums the
@@ -610,16 +588,14 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     s_rank[q] = flag;
                 }
                 __syncthreads();
-                STAMP(4);
                 // ---- stage 3: ranks of kept entries = tile-local output positions; look-back
                 const uint32_t tile_c = lds_excl_scan(s_rank, P_t, s_wsum);
                 if (tid < 64) {
                     const unsigned long long g =
-                        lookback_wave(states, tile, tile_c, ws, defer_polls, true, defer_ticks, cbase);
+                        lookback_wave(states, tile, tile_c, ws, defer_polls, true, defer_ticks);
                     if (tid == 0) s_off = g;
                 }
                 __syncthreads();
-                STAMP(5);
                 if (s_off == ~0ull) {  // uniform: no prefix yet -> take pool space, or wait
                     if (tid == 0) {
                         const unsigned long long o = atomicAdd(&ws->pool_used, (unsigned long long)tile_c);
@@ -632,7 +608,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     __syncthreads();
                     if (s_pool == ~0ull) {
                         if (tid < 64) {
-                            const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, false, 0, cbase);
+                            const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, false, 0);
                             if (tid == 0) s_off = g;
                         }
                         __syncthreads();
@@ -679,21 +655,19 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     Cp[n_rows] = (OP)(G + tile_c);
                     ws->total = G + tile_c;
                 }
-                STAMP(6);
                 return;
             }
         }
         __syncthreads();
     }
     // ---- exact slow path (uniform branch)
-    STAMP(7);
     uint32_t* s_rowc = reinterpret_cast<uint32_t*>(lds + heavy_lds_bytes(p, sizeof(T)) - 4 * kBlock);
     heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 0, 0,
                                   Cp, Cj, Cx, false, order);
     uint32_t tile_c;
     (void)block_excl_scan(tid < nrows ? s_rowc[tid] : 0u, s_wsum, &tile_c);
     if (tid < 64) {
-        const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, true, 0, cbase);
+        const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, true, 0);
         if (tid == 0) s_off = g;
     }
     __syncthreads();
@@ -713,11 +687,11 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
 // load flavour (profiles/r01_probe_gather_*.json). Staging turns them into L2 hits plus streams: the
 // tile's entries are partitioned by column bucket (2^sb features = a W32 slice of 4 * 2^sb bytes),
 // each bucket's words gathered on one XCD whose 4 MB L2 holds the slice, and the descriptors put
-// back into entry order. (The tile pipeline's own staged gather, measured slower than its direct
-// gathers in every configuration, was removed in round 4.)
+// back into entry order by the wave kernel. (The tile pipeline's own staged gather, measured slower
+// than its direct gathers in every configuration, was removed in round 4.)
 // W32 word of feature j (built from W): bits 30-31 = n if the R row has n <= 2 entries, the low
-// 30 bits then hold W's slots 0-1 unchanged; n = 3 marks "more": the low 30 bits are j itself and
-// the main kernel takes the full word from W (2% of KDD2012 features).
+// 30 bits then hold W's slots 0-1 unchanged; n = 3 marks "more": the count and the feature's index
+// in the side table SW, whose word the wave kernel fetches (4% of KDD2012 features).
 constexpr int kStageMaxNB = 256;  // buckets (one per thread in the partition scan)
 
 // bit j of BM = feature j has at least one R entry (57% of KDD2012 features have none)
@@ -730,48 +704,66 @@ __global__ void build_bitmap_kernel(const uint64_t* __restrict__ W, uint32_t* __
     }
 }
 
-// set bits of a bitmap (one atomicAdd per workgroup)
-__global__ void count_bits_kernel(const uint32_t* __restrict__ BM, int64_t words, unsigned long long* __restrict__ out) {
-    __shared__ unsigned long long s_n;
+// Side table: the W words of the features with more than 2 R entries (4.1% of KDD2012's features,
+// 1.9% of its A entries), packed in feature order (SW[k] = W[j] for the k-th such feature j). A W32
+// code-3 word carries k instead of j, so the row-lane kernels fetch those words from an 8 MB table
+// (MALL-resident, partly L2) instead of a random line of the 437 MB W. Built in two passes over
+// 1024-feature blocks: counts, then (after an inclusive scan of the counts) the words.
+constexpr int kSideBlock = 1024;
+__global__ void __launch_bounds__(kSideBlock)
+side_count_kernel(const uint64_t* __restrict__ W, int64_t m, int64_t* __restrict__ cnt) {
+    __shared__ uint32_t s_n;
     if (threadIdx.x == 0) s_n = 0;
     __syncthreads();
-    unsigned long long c = 0;
-    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < words; k += (int64_t)gridDim.x * blockDim.x)
-        c += (unsigned)__popc(BM[k]);
-    atomicAdd(&s_n, c);
+    const int64_t j = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
+    const bool side = j < m && (W[j] >> 61) > 2;
+    const uint64_t b = __ballot(side);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&s_n, (uint32_t)__popcll(b));
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(out, s_n);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = s_n;
 }
 
-// W32 word of a feature with more than 2 R entries: code 3, its entry count (4 bits, 15 = "15 or
-// more") and j (26 bits: staging needs m <= 2^26), so the row-lane kernel knows every entry's
-// product count without the dependent W gather
-__global__ void build_w32_kernel(const uint64_t* __restrict__ W, const uint16_t* __restrict__ O,
-                                 uint32_t* __restrict__ W32, int64_t m) {
-    for (int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; j < m;
-         j += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t w = W[j];
-        const uint32_t n = (uint32_t)(w >> 61);
-        const uint32_t cnt = n != 7 ? n : O[w & kLow61];
-        W32[j] = n <= 2 ? ((n << 30) | (uint32_t)(w & 0x3fffffffu))
-                        : (0xc0000000u | (std::min(cnt, 15u) << 26) | (uint32_t)j);
-    }
+// W32 word of feature j: n <= 2 entries inline (the low 30 bits of W); more: code 3, the entry
+// count (4 bits, 15 = "15 or more") and the side index k (26 bits: staging needs m <= 2^26), so
+// the row-lane kernels know every entry's product count without the side gather. cnt_incl = the
+// inclusive scan of side_count_kernel's counts.
+__global__ void __launch_bounds__(kSideBlock)
+build_w32_kernel(const uint64_t* __restrict__ W, const uint16_t* __restrict__ O, const int64_t* __restrict__ cnt_incl,
+                 uint32_t* __restrict__ W32, uint64_t* __restrict__ SW, int64_t m) {
+    __shared__ uint32_t s_wsum[kSideBlock / 64];
+    const int64_t j = (int64_t)blockIdx.x * kSideBlock + threadIdx.x;
+    const uint64_t w = j < m ? W[j] : 0ull;
+    const uint32_t n = (uint32_t)(w >> 61);
+    const bool side = n > 2;
+    const uint64_t b = __ballot(side);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) s_wsum[wv] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t k = (uint32_t)(blockIdx.x ? cnt_incl[blockIdx.x - 1] : 0) +
+                 (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
+    for (int i = 0; i < wv; ++i) k += s_wsum[i];
+    if (j >= m) return;
+    if (side) SW[k] = w;
+    const uint32_t cnt = n != 7 ? n : O[w & kLow61];
+    W32[j] = n <= 2 ? ((n << 30) | (uint32_t)(w & 0x3fffffffu)) : (0xc0000000u | (std::min(cnt, 15u) << 26) | k);
 }
 
 
 // ---- staging for the row-lane pipeline: bucket-major runs inside groups of kRunGroup tiles.
 // S holds, for tile group g and bucket b, the entries of all the group's tiles whose feature falls
-// in b as ONE contiguous segment (one run per tile, runs in claim order, rank order inside the
-// run); segments are laid out in (g, b) order, each with a reserve sized from the group's entries
-// (lpr_reserve_kernel). So the gather streams whole segments (full 128-byte lines, nothing shared
-// between workgroups), and a tile's entries come back as nb runs. One pass over A (the partition
-// claims the runs of a super-tile of four tiles with one atomicAdd per bucket on its segment's
-// fill); a segment past its reserve (columns far from uniform) sends the call to the direct
-// kernel. Index arrays (workspace, tile-major: a tile's table is contiguous):
-//   OFFT[t][b] (u16)  within-tile start of bucket b (bucket order), OFFT[t][nb] = the tile's entries
-//   OFF2[t][b] (u32)  start of tile t's run in segment (g, b), relative to the segment
-//   GB[g*nb + b] (i64) segment start in S (exclusive prefix of the reserves), FILL[g*nb + b] its fill
-// A tile past the entry cap stages nothing (its counts are 0): the heavy path reads A itself.
+// in b as ONE contiguous segment (one run per tile, runs in claim order); segments are laid out in
+// (g, b) order, each with a reserve sized from the group's entries (lpr_reserve_kernel). Inside a
+// tile's run the entries are grouped by 64-row unit (unit 0's first, any order inside a unit), so
+// each wave of the wave kernel reads its own unit's part of every run. The gather streams whole
+// segments (full 128-byte lines, nothing shared between workgroups). One pass over A (the
+// partition claims the runs of a super-tile of kPartTiles tiles with one atomicAdd per bucket on
+// its segment's fill); a segment past its reserve (columns far from uniform) sends the rest of the
+// call to direct gathers. Index arrays (workspace, tile-major: a tile's table is contiguous):
+//   OFF2[t][b] (u32)     start of tile t's run in segment (g, b), relative to the segment
+//   CU[t][u - 1][b] (u16) entries of bucket b in units < u of tile t, u = 1..4 (u = 4: the run)
+//   GB[g*nb + b] (i64)   segment start in S (exclusive prefix of the reserves), FILL[g*nb + b] its fill
+// S word: the entry's index in its tile << 20 | its feature's bits inside the bucket. A tile past
+// the entry cap stages nothing (its counts are 0): the heavy path reads A itself.
 constexpr int kRunGroup = 4096;  // tiles per group (uniform KDD2012: ~110K entries per segment)
 
 // XCD-aware tile order: workgroup i runs on XCD i % 8 (round-robin dispatch); XCD x takes tiles
@@ -867,29 +859,37 @@ __device__ __forceinline__ uint32_t run_of(const uint16_t* st, int nb, uint32_t 
     return lo;
 }
 
-// K2: partition, one workgroup per SUPER-TILE of kPartTiles = 4 consecutive tiles (one 256-thread
-// quarter per tile). Each tile's entries are histogrammed by bucket in LDS, its within-tile bucket
-// starts go to OFFT, and ONE atomicAdd per bucket on FILL claims the (group, bucket) segment room of
-// all four tiles at once: the four runs of a bucket are adjacent in their segment, in tile order
-// (OFF2 = each run's position), so the unsort pass reads a super-tile's runs of a bucket as one
-// contiguous range and the S stores of a bucket fill whole lines inside one workgroup. The entries
-// are ranked into bucket order in LDS and written to their runs (consecutive lanes -> consecutive S
-// words). S word: entry index in the tile << 20 | column bits. A run past its segment's reserve
-// sets the gate to 0: the call's remaining kernels take the direct path (lpr_main_flat_kernel). A
-// tile past the entry cap stages nothing (its counts are 0): the heavy path reads A itself.
+// K2: partition, one workgroup per SUPER-TILE of kPartTiles consecutive tiles (one 256-thread
+// part per tile). Each tile's entries are histogrammed by (unit, bucket) in LDS; the unit counts
+// give CU and each entry's place inside its tile's run of a bucket (its unit's part: a cursor per
+// (unit, bucket), ranked with one LDS atomic), the bucket starts give the tile's bucket-ordered
+// layout. ONE atomicAdd per bucket on FILL claims the segment room of the super-tile's runs at once:
+// its tiles' runs of a bucket are adjacent in their segment, in tile order (OFF2 = each run's
+// position), so the S stores of a bucket fill whole lines inside one workgroup and the wave kernel
+// reads neighbouring units' parts of a run from lines its XCD's L2 already holds. The entries are
+// ranked into bucket order in LDS and written to their runs (consecutive lanes -> consecutive S
+// words). A run past its segment's reserve sets the gate to 0: the call's remaining kernels take
+// direct gathers. A tile past the entry cap stages nothing (its counts are 0).
 constexpr int kPartTiles = 2;
 constexpr int kPBlock = kBlock * kPartTiles;
 static_assert(kRunGroup % kPartTiles == 0, "a super-tile never straddles two groups");
+// dynamic LDS: [the ranked S words [kPartTiles][cap_a], aliased by the unit histograms
+// [kPartTiles][4][nb] (dead by then)] [cursors [kPartTiles][4][nb]] [run destinations
+// [kPartTiles][nb] (i64)] [bucket starts [kPartTiles][nb + 1] (u16)]
+__host__ __device__ inline size_t lpr_partition_keys_bytes(int cap_a, int nb) {
+    return (std::max<size_t>(4 * (size_t)kPartTiles * (size_t)cap_a, 16 * (size_t)kPartTiles * (size_t)nb) + 15) & ~size_t(15);
+}
+__host__ __device__ inline size_t lpr_partition_lds_bytes(int cap_a, int nb) {
+    return lpr_partition_keys_bytes(cap_a, nb) + 16 * (size_t)kPartTiles * nb + 8 * (size_t)kPartTiles * nb +
+           ((2 * (size_t)kPartTiles * (nb + 1) + 15) & ~size_t(15));
+}
 template <typename IP>
 __global__ void __launch_bounds__(kPBlock)
-lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, Caps caps,
-                     unsigned n_tiles, unsigned s8, int sb, int nb, uint32_t ostride, uint16_t* __restrict__ OFFT,
-                     uint32_t* __restrict__ OFF2, const int64_t* __restrict__ GB, uint32_t* __restrict__ FILL,
+lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, int cap_a,
+                     unsigned n_tiles, unsigned s8, int sb, int nb, uint32_t ostride, uint32_t* __restrict__ OFF2,
+                     uint16_t* __restrict__ CU, const int64_t* __restrict__ GB, uint32_t* __restrict__ FILL,
                      uint32_t* __restrict__ S, uint32_t* __restrict__ gate) {
-    extern __shared__ __align__(16) uint32_t s_key[];  // [kPartTiles][cap_a]
-    __shared__ uint32_t s_cur[kPartTiles][kStageMaxNB];
-    __shared__ uint16_t s_st[kPartTiles][kStageMaxNB + 1];
-    __shared__ int64_t s_dst[kPartTiles][kStageMaxNB];
+    extern __shared__ __align__(16) uint32_t s_key[];  // [kPartTiles][cap_a]; first the unit histograms
     __shared__ uint32_t s_wsum[kPBlock / 64];
     __shared__ int s_over;
     __shared__ uint32_t s_gate;
@@ -903,37 +903,59 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
     const unsigned t0 = xcd_tile(blockIdx.x, s8) * kPartTiles;
     if (t0 >= n_tiles) return;  // uniform
     const unsigned t = t0 + q;
-    const bool live = t < n_tiles;  // quarter-uniform
+    const bool live = t < n_tiles;  // part-uniform
+    unsigned char* dyn = reinterpret_cast<unsigned char*>(s_key) + lpr_partition_keys_bytes(cap_a, nb);
+    uint32_t* s_cur = reinterpret_cast<uint32_t*>(dyn);  // per (tile, unit, bucket): next slot in the layout
+    int64_t* s_dst = reinterpret_cast<int64_t*>(dyn + 16 * (size_t)kPartTiles * nb);  // per (tile, bucket)
+    uint16_t* s_st = reinterpret_cast<uint16_t*>(dyn + 24 * (size_t)kPartTiles * nb);  // per tile: nb + 1
     int64_t ea = 0, ne = 0;
+    uint32_t u1 = 0, u2 = 0, u3 = 0;  // first entries of units 1..3 (tile-relative)
     if (live) {
-        const int64_t row0 = (int64_t)t * caps.rpt;
+        const int64_t row0 = (int64_t)t * kBlock;
         ea = (int64_t)Ap[row0];
-        ne = (int64_t)Ap[std::min<int64_t>(row0 + caps.rpt, n_rows)] - ea;
+        ne = (int64_t)Ap[std::min<int64_t>(row0 + kBlock, n_rows)] - ea;
+        u1 = (uint32_t)((int64_t)Ap[std::min<int64_t>(row0 + 64, n_rows)] - ea);
+        u2 = (uint32_t)((int64_t)Ap[std::min<int64_t>(row0 + 128, n_rows)] - ea);
+        u3 = (uint32_t)((int64_t)Ap[std::min<int64_t>(row0 + 192, n_rows)] - ea);
     }
-    const uint32_t n = ne > caps.cap_a ? 0u : (uint32_t)ne;  // a heavy tile stages nothing: all runs empty
+    const uint32_t n = ne > cap_a ? 0u : (uint32_t)ne;  // a heavy tile stages nothing: all runs empty
     const int32_t* __restrict__ Ajt = Aj + ea;
-    int32_t jj[kMaxE];
+    int32_t jj[kMaxE];  // feature | unit << 27 (staging needs m <= 2^26), -1 past the tile
 #pragma unroll
     for (int i = 0; i < kMaxE; ++i) {
         const uint32_t e = qt + i * kBlock;
         jj[i] = e < n ? Ajt[e] : -1;
     }
-    if (qt < nb) s_cur[q][qt] = 0;
+    uint32_t* hu = s_key + (size_t)q * 4 * nb;  // unit histograms of this part's tile
+    for (int i = qt; i < 4 * nb; i += kBlock) hu[i] = 0u;
     if (tid == 0) s_over = 0;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kMaxE; ++i)
-        if (jj[i] >= 0) atomicAdd(&s_cur[q][(uint32_t)jj[i] >> sb], 1u);
+        if (jj[i] >= 0) {
+            const uint32_t e = qt + i * kBlock;
+            const uint32_t u = (e >= u1) + (e >= u2) + (e >= u3);
+            jj[i] |= (int32_t)(u << 27);
+            atomicAdd(&hu[u * nb + (((uint32_t)jj[i] & kW32J) >> sb)], 1u);
+        }
     __syncthreads();
-    const uint32_t cnt = qt < nb ? s_cur[q][qt] : 0u;
-    // the super-tile's claim of bucket qt (quarter 0): issued now, consumed after the ranking
+    uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+    if (qt < nb) {
+        h0 = hu[qt];
+        h1 = hu[nb + qt];
+        h2 = hu[2 * nb + qt];
+        h3 = hu[3 * nb + qt];
+    }
+    const uint32_t cnt = h0 + h1 + h2 + h3;
+    // the super-tile's claim of bucket qt (part 0): issued now, consumed after the ranking
     uint32_t claim = 0, c4[kPartTiles] = {}, tot4 = 0;
     int64_t lo = 0, hi = 0;
     const unsigned sg = (t0 / kRunGroup) * (unsigned)nb + (unsigned)qt;
     if (q == 0 && qt < nb) {
 #pragma unroll
         for (int k = 0; k < kPartTiles; ++k) {
-            c4[k] = s_cur[k][qt];
+            const uint32_t* hk = s_key + (size_t)k * 4 * nb;
+            c4[k] = hk[qt] + hk[nb + qt] + hk[2 * nb + qt] + hk[3 * nb + qt];
             tot4 += c4[k];
         }
         if (tot4 > 0) {
@@ -942,37 +964,46 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
             hi = GB[sg + 1];
         }
     }
-    // within-tile bucket starts: exclusive scan of cnt over the quarter's 256 threads
+    // within-tile bucket starts: exclusive scan of cnt over the part's 256 threads
     const uint32_t inc = wave_incl_scan(cnt);
     if ((tid & 63) == 63) s_wsum[w] = inc;
-    __syncthreads();
+    __syncthreads();  // also: every histogram read above is done (s_key is rewritten below)
     uint32_t st = inc - cnt;
     for (int i = 4 * q; i < w; ++i) st += s_wsum[i];
+    uint32_t* cur = s_cur + (size_t)q * 4 * nb;
     if (qt < nb) {
-        s_st[q][qt] = (uint16_t)st;
-        s_cur[q][qt] = st;
-        if (live) OFFT[(size_t)t * ostride + qt] = (uint16_t)st;
+        s_st[q * (nb + 1) + qt] = (uint16_t)st;
+        cur[qt] = st;
+        cur[nb + qt] = st + h0;
+        cur[2 * nb + qt] = st + h0 + h1;
+        cur[3 * nb + qt] = st + h0 + h1 + h2;
+        if (live) {
+            uint16_t* cu = CU + (size_t)t * 4 * ostride + qt;
+            cu[0] = (uint16_t)h0;
+            cu[ostride] = (uint16_t)(h0 + h1);
+            cu[2 * ostride] = (uint16_t)(h0 + h1 + h2);
+            cu[3 * ostride] = (uint16_t)cnt;
+        }
     }
-    if (qt == 0) {
-        s_st[q][nb] = (uint16_t)n;
-        if (live) OFFT[(size_t)t * ostride + nb] = (uint16_t)n;
-    }
+    if (qt == 0) s_st[q * (nb + 1) + nb] = (uint16_t)n;
     __syncthreads();
     const uint32_t mask = (1u << sb) - 1u;
-    uint32_t* sk = s_key + (size_t)q * caps.cap_a;
+    uint32_t* sk = s_key + (size_t)q * cap_a;
 #pragma unroll
     for (int i = 0; i < kMaxE; ++i)
         if (jj[i] >= 0) {
-            const uint32_t pos = atomicAdd(&s_cur[q][(uint32_t)jj[i] >> sb], 1u);
-            sk[pos] = ((qt + i * kBlock) << 20) | ((uint32_t)jj[i] & mask);
+            const uint32_t e = qt + i * kBlock;
+            const uint32_t f = (uint32_t)jj[i] & kW32J;
+            const uint32_t pos = atomicAdd(&cur[((uint32_t)jj[i] >> 27) * nb + (f >> sb)], 1u);
+            sk[pos] = (e << 20) | (f & mask);
         }
-    if (q == 0 && qt < nb) {  // the four tiles' runs of bucket qt, adjacent in tile order
+    if (q == 0 && qt < nb) {  // the super-tile's runs of bucket qt, adjacent in tile order
         uint32_t run = claim;
         if (tot4 > 0 && lo + (int64_t)claim + tot4 > hi) s_over = 1;
 #pragma unroll
         for (int k = 0; k < kPartTiles; ++k) {
             if (t0 + k < n_tiles) {
-                s_dst[k][qt] = lo + (int64_t)run - (int64_t)s_st[k][qt];
+                s_dst[k * nb + qt] = lo + (int64_t)run - (int64_t)s_st[k * (nb + 1) + qt];
                 OFF2[(size_t)(t0 + k) * ostride + qt] = run;
             }
             run += c4[k];
@@ -983,10 +1014,11 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
         if (tid == 0) *gate = 0;
         return;
     }
-    for (uint32_t pos = qt; pos < n; pos += kBlock) S[s_dst[q][run_of(s_st[q], nb, pos)] + pos] = sk[pos];
+    const uint16_t* stq = s_st + q * (nb + 1);
+    for (uint32_t pos = qt; pos < n; pos += kBlock) S[s_dst[q * nb + run_of(stq, nb, pos)] + pos] = sk[pos];
 }
 
-// K3: filtered gather, one workgroup per (bucket b, group g) segment, on XCD b % 8 (workgroup i
+// K3: gather, one workgroup per (bucket b, group g) segment, on XCD b % 8 (workgroup i
 // runs on XCD i % 8, so one XCD's CUs work on one bucket at a time and its L2 holds that W32
 // slice). The bucket's nonempty-feature bitmap (2^sb bits) is staged in LDS: an entry whose R row
 // is empty (57% of KDD2012 entries) gets D = 0 without an L2 request, the others gather their
@@ -1079,207 +1111,6 @@ defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsi
         }
         __syncthreads();
     }
-}
-
-// ------------------------------------------------------------------------------------------
-// Filtered tile pipeline (long rows over an R with mostly empty rows — configs[3]:
-// 72% of the 10M features have no R entry, yet every A entry gathered its W word, 2.0e10 random
-// lines at the ~55 G lines/s fabric ceiling). A streaming pass drops the A entries whose feature
-// has an empty R row (a 1-bit-per-feature bitmap, L2-resident: 1.25 MB for m = 10M) and writes the
-// rest as a compact CSR A' (int32 row pointers, same entry order); the tile kernel then runs on A'.
-// Exact: an entry with an empty R row contributes no product to scipy's csr_matmat (no first touch,
-// no sum), so A' @ R == A @ R bit for bit, order included. Launches are cut into row chunks of at
-// most `emax` entries (A' is sized for one chunk); chunk k's tile 0 starts at the running total of
-// chunks < k (ws->total, see lookback_wave's base0).
-constexpr int kFiltSteps = 16;                      // 256 x 16 entries per round, in registers
-constexpr int kFiltRound = kBlock * kFiltSteps;
-constexpr int kFiltProbe = 4096;                    // row-pointer probes (chunk boundaries)
-constexpr int kFiltSample = 65536;                  // entries sampled for the kept fraction
-
-// kept-entry mask of unit u (one u64 per 64 of its entries, from its own first entry): at word
-// floor(first entry / 64) + u of the chunk's mask, so units never share a word
-__host__ __device__ inline int64_t filter_mask_base(int64_t ea_rel, unsigned unit) { return ea_rel / 64 + unit; }
-
-__device__ __forceinline__ bool bm_test(const uint32_t* __restrict__ BM, int32_t j) {
-    return (BM[(uint32_t)j >> 5] >> (j & 31)) & 1u;
-}
-
-// one workgroup: Ap at kFiltProbe + 1 evenly spaced rows (out[0..K]) and, over kFiltSample evenly
-// spaced entries, how many have a nonempty R row (out[K + 1])
-template <typename IP>
-__global__ void __launch_bounds__(1024)
-filter_probe_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows,
-                    const uint32_t* __restrict__ BM, int64_t* __restrict__ out) {
-    __shared__ uint32_t s_kept;
-    if (threadIdx.x == 0) s_kept = 0;
-    __syncthreads();
-    for (int k = threadIdx.x; k <= kFiltProbe; k += blockDim.x)
-        out[k] = (int64_t)Ap[n_rows * k / kFiltProbe];  // (n_rows < 2^40)
-    const int64_t e0 = (int64_t)Ap[0], ne = (int64_t)Ap[n_rows] - e0;
-    uint32_t kept = 0;
-    if (ne > 0)
-        for (int s = threadIdx.x; s < kFiltSample; s += blockDim.x)
-            kept += bm_test(BM, Aj[e0 + ne / kFiltSample * s + ne % kFiltSample * s / kFiltSample]) ? 1u : 0u;
-    atomicAdd(&s_kept, kept);
-    __syncthreads();
-    if (threadIdx.x == 0) out[kFiltProbe + 1] = s_kept;
-}
-
-// A' positions without a look-back (a decoupled look-back over 630K units per chunk measured 16 ms
-// per chunk: its waiting polls, not the 8.6 GB streamed, bound it): (1) filter_count_kernel, one
-// workgroup per unit of `rpu` rows, counts the unit's kept entries; (2) filter_scan_kernel: per
-// block of 4096 units the local exclusive scan and the block's sum, then (3) filter_scan_top_kernel
-// scans the block sums; (4) filter_write_kernel re-reads the unit's entries and writes the kept
-// ones at boff[unit / 4096] + uoff[unit], in entry order (per 256-entry step: wave ballot ranks +
-// the round's (step, wave) prefix), and the row pointers Fp from the same prefixes.
-template <typename IP>
-__global__ void __launch_bounds__(kBlock)
-filter_count_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, int64_t n_rows, int rpu,
-                    const uint32_t* __restrict__ BM, uint32_t* __restrict__ ucnt, uint64_t* __restrict__ kmask) {
-    __shared__ uint32_t s_wsum[kBlock / 64];
-    const unsigned unit = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t row0 = (int64_t)unit * rpu;
-    const int nr = (int)std::min<int64_t>(rpu, n_rows - row0);
-    const int64_t e0 = (int64_t)Ap[0], ea = (int64_t)Ap[row0];
-    const uint32_t n = (uint32_t)((int64_t)Ap[row0 + nr] - ea);  // < 2^31 (chunks of <= emax entries)
-    const int32_t* __restrict__ Aju = Aj + ea;
-    uint64_t* __restrict__ km = kmask + filter_mask_base(ea - e0, unit);
-    uint32_t mine = 0;
-    for (uint32_t b = 0; b < n; b += kFiltRound) {
-        int32_t jv[kFiltSteps];
-#pragma unroll
-        for (int i = 0; i < kFiltSteps; ++i) {
-            const uint32_t e = b + i * kBlock + tid;
-            jv[i] = e < n ? __builtin_nontemporal_load(Aju + e) : -1;
-        }
-#pragma unroll
-        for (int i = 0; i < kFiltSteps; ++i) {
-            const bool kp = jv[i] >= 0 && bm_test(BM, jv[i]);
-            mine += kp ? 1u : 0u;
-            const uint64_t bal = __ballot(kp);
-            if (lane == 0 && b + i * kBlock + w * 64 < n) km[(b + i * kBlock) / 64 + w] = bal;
-        }
-    }
-    uint32_t total;
-    (void)block_excl_scan(mine, s_wsum, &total);
-    if (tid == 0) ucnt[unit] = total;
-}
-
-constexpr int kFiltScanPer = 16;                            // units per thread in filter_scan_kernel
-constexpr int kFiltScanBlock = kBlock * kFiltScanPer;       // 4096 units per scan block
-
-__global__ void __launch_bounds__(kBlock)
-filter_scan_kernel(const uint32_t* __restrict__ ucnt, unsigned n_units, uint32_t* __restrict__ uoff,
-                   uint32_t* __restrict__ bsum) {
-    __shared__ uint32_t s_wsum[kBlock / 64];
-    const size_t u0 = (size_t)blockIdx.x * kFiltScanBlock + (size_t)threadIdx.x * kFiltScanPer;
-    uint32_t v[kFiltScanPer], run = 0;
-#pragma unroll
-    for (int i = 0; i < kFiltScanPer; ++i) {
-        v[i] = u0 + i < n_units ? ucnt[u0 + i] : 0u;
-        run += v[i];
-    }
-    uint32_t total;
-    uint32_t ex = block_excl_scan(run, s_wsum, &total);
-#pragma unroll
-    for (int i = 0; i < kFiltScanPer; ++i) {
-        if (u0 + i < n_units) uoff[u0 + i] = ex;
-        ex += v[i];
-    }
-    if (threadIdx.x == 0) bsum[blockIdx.x] = total;
-}
-
-// one workgroup of 1024 threads: exclusive scan of the nb <= 16384 scan-block sums
-__global__ void __launch_bounds__(1024)
-filter_scan_top_kernel(const uint32_t* __restrict__ bsum, unsigned nb, uint32_t* __restrict__ boff) {
-    __shared__ uint32_t s_w[16];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    uint32_t v[16], run = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        v[i] = (unsigned)(tid * 16 + i) < nb ? bsum[tid * 16 + i] : 0u;
-        run += v[i];
-    }
-    const uint32_t inc = wave_scan_dpp(run);
-    if (lane == 63) s_w[w] = inc;
-    __syncthreads();
-    uint32_t ex = inc - run;
-    for (int i = 0; i < w; ++i) ex += s_w[i];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if ((unsigned)(tid * 16 + i) < nb) boff[tid * 16 + i] = ex;
-        ex += v[i];
-    }
-}
-
-template <typename T, typename IP>
-__global__ void __launch_bounds__(kBlock)
-filter_write_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
-                    int64_t n_rows, int rpu, unsigned n_units, const uint64_t* __restrict__ kmask,
-                    const uint32_t* __restrict__ ucnt, const uint32_t* __restrict__ uoff,
-                    const uint32_t* __restrict__ boff, int32_t* __restrict__ Fp, int32_t* __restrict__ Fj,
-                    T* __restrict__ Fx) {
-    __shared__ uint64_t s_bal[kFiltSteps][kBlock / 64];
-    __shared__ uint32_t s_pre[kFiltSteps * (kBlock / 64)];
-    __shared__ uint32_t s_rtot;
-    const unsigned unit = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t row0 = (int64_t)unit * rpu;
-    const int nr = (int)std::min<int64_t>(rpu, n_rows - row0);
-    const int64_t e0 = (int64_t)Ap[0], ea = (int64_t)Ap[row0];
-    const uint32_t n = (uint32_t)((int64_t)Ap[row0 + nr] - ea);
-    const uint32_t er = tid < nr ? (uint32_t)((int64_t)Ap[row0 + tid] - ea) : 0u;  // row tid's first entry
-    const uint32_t G = boff[unit / kFiltScanBlock] + uoff[unit];
-    const uint64_t* __restrict__ km = kmask + filter_mask_base(ea - e0, unit);
-    const int32_t* __restrict__ Aju = Aj + ea;
-    const T* __restrict__ Axu = Ax + ea;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t rbase = 0;  // kept entries of earlier rounds
-    for (uint32_t b = 0; b < n; b += kFiltRound) {
-        int32_t jv[kFiltSteps];
-        T xv[kFiltSteps];
-#pragma unroll
-        for (int i = 0; i < kFiltSteps; ++i) {
-            const uint32_t e = b + i * kBlock + tid;
-            jv[i] = e < n ? __builtin_nontemporal_load(Aju + e) : -1;
-            xv[i] = e < n ? __builtin_nontemporal_load(Axu + e) : T(0);
-        }
-        bool kp[kFiltSteps];
-#pragma unroll
-        for (int i = 0; i < kFiltSteps; ++i) {  // the count pass's ballots (one wave-uniform word)
-            const uint64_t bal = b + i * kBlock + w * 64 < n ? km[(b + i * kBlock) / 64 + w] : 0ull;
-            kp[i] = (bal >> lane) & 1ull;
-            if (lane == 0) s_bal[i][w] = bal;
-        }
-        __syncthreads();
-        static_assert(kFiltSteps * (kBlock / 64) <= 64, "one wave scans the (step, wave) counts");
-        if (tid < 64) {  // exclusive prefix over (step, wave) in entry order: lane = step * 4 + wave
-            const uint32_t c = tid < kFiltSteps * (kBlock / 64)
-                                   ? (uint32_t)__builtin_popcountll(s_bal[tid >> 2][tid & 3]) : 0u;
-            const uint32_t inc = wave_scan_dpp(c);
-            if (tid < kFiltSteps * (kBlock / 64)) s_pre[tid] = inc - c;
-            if (tid == kFiltSteps * (kBlock / 64) - 1) s_rtot = inc;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < kFiltSteps; ++i)
-            if (kp[i]) {
-                const uint32_t o = G + rbase + s_pre[i * 4 + w] + (uint32_t)__builtin_popcountll(s_bal[i][w] & lt);
-                Fj[o] = jv[i];
-                Fx[o] = xv[i];
-            }
-        // row pointers of the rows starting in this round
-        if (tid < nr && er >= b && er < b + kFiltRound && er < n) {
-            const uint32_t t = er - b, i = t >> 8, ww = (t >> 6) & 3, l = t & 63;
-            Fp[row0 + tid] = (int32_t)(G + rbase + s_pre[i * 4 + ww] +
-                                       (uint32_t)__builtin_popcountll(s_bal[i][ww] & ((1ull << l) - 1ull)));
-        }
-        rbase += s_rtot;
-        __syncthreads();  // s_bal / s_pre / s_rtot reused by the next round
-    }
-    if (tid < nr && er >= n) Fp[row0 + tid] = (int32_t)(G + ucnt[unit]);  // rows starting at the unit's end
-    if (unit == n_units - 1 && tid == 0) Fp[row0 + nr] = (int32_t)(G + ucnt[unit]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1404,10 +1235,10 @@ __device__ __forceinline__ T wave_incl_scan_t(T v, int lane) {
 
 // staged runs of the row-lane pipeline (see lpr_partition_kernel)
 struct LprStage {
-    const uint32_t* gate;  // non-NULL: staged iff *gate (lpr_choose_kernel); the direct kernel iff !*gate
-    const uint32_t* w32;   // direct gathers from the 4-byte W32 table (NULL: the 8-byte W words)
-    const uint16_t* offt;
+    const uint32_t* gate;  // staged iff *gate (a segment overflow in the partition clears it)
+    const uint32_t* w32;   // W32 table: direct gathers (NULL: the 8-byte W words)
     const uint32_t* off2;
+    const uint16_t* cu;
     const int64_t* gb;
     const uint32_t* s;
     const uint32_t* d;
@@ -1415,491 +1246,19 @@ struct LprStage {
     int nb;
 };
 
-// Persistent and software-pipelined: a workgroup walks the tiles k = blockIdx.x, + gridDim.x, ...
-// (gridDim.x a multiple of 8, so all of a workgroup's tiles are in its XCD's range, xcd_tile) and
-// overlaps the memory rounds of tile k + 1 with the compute of tile k. Per tile:
-//   round 1 (only the tile index): row pointers and, staged, the tile's run table — issued before
-//            the flat pass of the previous tile;
-//   round 2 (needs round 1): staged, the S/D words of every run; direct, the feature ids (and the
-//            W gathers at the top of the tile's own iteration) — issued before the previous
-//            tile's row phase, with the first values of the flat pass;
-// so a tile's compute waits on memory only where round 2 outlasts the previous tile's row phase.
-template <typename T, typename IP, bool STAGED>
-__global__ void __launch_bounds__(kLprRows) __attribute__((amdgpu_waves_per_eu(4)))
-lpr_main_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
-                const T* __restrict__ Ax, LprStage stg, int cap_a, unsigned n_tiles, unsigned t8, int order,
-                LprSpace sp, Workspace* ws) {
-    extern __shared__ __align__(16) unsigned char lds[];          // s_desc[cap_a] u32, 4 slots
-    __shared__ uint16_t s_rowptr[kLprRows + 1];
-    __shared__ uint64_t s_side[kLprSide];
-    __shared__ uint32_t s_sidej[kLprSide];                          // side entry's feature (staged)
-    __shared__ uint16_t s_sfk[kLprSide];                            // side entry's slot position
-    __shared__ uint8_t s_sfw[kLprSide];                             // ... in the slot of this wave
-    __shared__ T s_sfx[kLprSide];                                   // ... and its value
-    __shared__ uint64_t s_flag[4][kLprFlagWords];                  // row-start bitmap per wave
-    __shared__ uint64_t s_susp[4];                                  // rows flagged for the exact path
-    __shared__ uint16_t s_kst[4][64];
-    __shared__ uint8_t s_nz2row[4][64];
-    // side-entry count and the heavy flag, one pair per iteration parity: the next tile's pair is
-    // reset after the barrier that ends every read of it in the tile before
-    __shared__ uint32_t s_nside[2], s_wnz[4];
-    __shared__ int s_bad[2];
-    // the NEXT tile's run table (staged): element -> run, see stage_runs below
-    __shared__ uint32_t s_ksrc[STAGED ? kStageMaxNB : 1];
-    __shared__ uint64_t s_sbm[STAGED ? 64 : 1];
-    uint32_t* s_desc = reinterpret_cast<uint32_t*>(lds);
-    uint16_t* s_colbuf = reinterpret_cast<uint16_t*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)));  // 4 x slot
-    T* s_valbuf = reinterpret_cast<T*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)) +
-                                       ((8 * (size_t)sp.slot + 15) & ~size_t(15)));                // 4 x slot
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-    const int wu = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const unsigned kend = 8u * t8;
-    constexpr int kU = 12;  // round-2 words per thread held across the previous tile's row phase
-
-    // ---- round 1 of a tile: raw loads into registers (consumed one phase later)
-    struct Pre {
-        unsigned tile;
-        int nrows;
-        IP a0, an, ae0, ae1, arp0, arp1;
-        int64_t g0, gbt;
-        uint16_t st0, st1;
-        uint32_t off2;
-    };
-    auto round1 = [&](unsigned k) {
-        Pre p{};
-        p.tile = k < kend ? xcd_tile(k, t8) : n_tiles;
-        if (p.tile >= n_tiles) return p;  // uniform
-        const int64_t row0 = (int64_t)p.tile * kLprRows;
-        p.nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
-        p.a0 = Ap[row0];
-        p.an = Ap[row0 + p.nrows];
-        p.ae0 = Ap[row0 + std::min(64 * wu, p.nrows)];
-        p.ae1 = Ap[row0 + std::min(64 * wu + 64, p.nrows)];
-        p.arp0 = tid <= p.nrows ? Ap[row0 + tid] : IP(0);
-        p.arp1 = tid == 0 && p.nrows == kLprRows ? Ap[row0 + kLprRows] : IP(0);
-        if constexpr (STAGED) {
-            const size_t gb = (size_t)(p.tile / kRunGroup) * stg.nb;
-            p.g0 = stg.gb[gb];
-            if (tid < stg.nb) {
-                const size_t o = (size_t)p.tile * stg.ostride + tid;  // the tile's run table: contiguous
-                p.st0 = stg.offt[o];
-                p.st1 = stg.offt[o + 1];
-                p.gbt = stg.gb[gb + tid];
-                p.off2 = stg.off2[o];
-            }
-        }
-        return p;
-    };
-    // ---- round 2 of a tile: staged S/D words (run lookup in s_ksrc / s_sbm) or direct feature ids,
-    // plus the first four value steps of the flat pass
-    uint32_t sv[kU], dv[kU];
-    constexpr int kXP = 4;  // flat-pass value steps in flight (loaded ahead of use; 8 spills: slower)
-    T xn[kXP];
-    auto run_lookup = [&](uint32_t q, uint32_t pre) {  // index of element q's word, relative to g0
-        const uint32_t k = (uint32_t)__shfl((int)pre, (int)(q >> 6), 64) +
-                           (uint32_t)__popcll(s_sbm[q >> 6] & (~0ull >> (63 - (q & 63)))) - 1u;
-        return s_ksrc[k & (kStageMaxNB - 1)] + q;  // (an element outside every run is never loaded)
-    };
-    auto round2 = [&](const Pre& p, uint32_t b0, uint32_t pre) {  // words [b0, b0 + kU * 256) of the tile
-        const uint32_t ne_all = (uint32_t)((int64_t)p.an - (int64_t)p.a0);
-        // a tile past cap_a staged nothing (its run table is empty): no words to fetch — the run
-        // lookup of an element outside every run would index s_ksrc[-1]
-        const uint32_t ne = ne_all > (uint32_t)cap_a ? 0u : ne_all;
-        if constexpr (STAGED) {
-            const uint32_t* __restrict__ St = stg.s + p.g0;
-            const uint32_t* __restrict__ Dt = stg.d + p.g0;
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {  // block-uniform trip count: every lane takes part in the shuffle
-                const uint32_t q0 = b0 + tid + u * kLprRows;
-                const uint32_t i = run_lookup(std::min(q0, ne - 1), pre);
-                sv[u] = q0 < ne ? St[i] : 0u;
-                dv[u] = q0 < ne ? Dt[i] : 0u;
-            }
-        } else {
-            const int32_t* __restrict__ Ajt = Aj + (int64_t)p.a0;
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const uint32_t e = b0 + tid + u * kLprRows;
-                sv[u] = e < ne ? (uint32_t)Ajt[e] : 0xffffffffu;
-            }
-        }
-    };
-    auto first_values = [&](const Pre& p) {
-        const int64_t ea = (int64_t)p.a0;
-        const uint32_t E0 = (uint32_t)((int64_t)p.ae0 - ea), E1 = (uint32_t)((int64_t)p.ae1 - ea);
-        const T* __restrict__ Axw = Ax + ea;
-        const uint32_t elast = E1 > E0 ? E1 - 1 : E0;
-#pragma unroll
-        for (int j = 0; j < kXP; ++j) {
-            const uint32_t e = E0 + 64 * j + lane;
-            const T v = Axw[std::min(e, elast)];
-            xn[j] = e < E1 ? v : T(0);
-        }
-    };
-    // staged: the run table of a tile into s_ksrc / s_sbm; returns this lane's `pre` (set bits in the
-    // start-bitmap words below word `lane`). Two block barriers.
-    auto stage_runs = [&](const Pre& p) -> uint32_t {
-        if constexpr (STAGED) {
-            const uint32_t m_st = p.st0, m_len = tid < stg.nb ? (uint32_t)p.st1 - (uint32_t)p.st0 : 0u;
-            const uint32_t m_src = (uint32_t)(p.gbt - p.g0) + p.off2;
-            if (tid < 64) s_sbm[tid] = 0ull;
-            const uint64_t nzb = __ballot(m_len > 0);
-            if (lane == 0) s_wnz[w] = (uint32_t)__popcll(nzb);
-            __syncthreads();
-            if (m_len > 0) {
-                uint32_t k = (uint32_t)__popcll(nzb & ((1ull << lane) - 1ull));
-                for (int i = 0; i < w; ++i) k += s_wnz[i];
-                s_ksrc[k] = m_src - m_st;
-                atomicOr(reinterpret_cast<unsigned long long*>(&s_sbm[m_st >> 6]), 1ull << (m_st & 63));
-            }
-            __syncthreads();
-            const uint32_t c = (uint32_t)__popcll(s_sbm[lane]);
-            return wave_scan_dpp(c) - c;
-        } else {
-            return 0u;
-        }
-    };
-    // descriptors of words [b0, b0 + kU * 256) into s_desc: the W32 word (n <= 2 entries inline);
-    // more entries -> code 3 | count << 26 | side index, the feature's W word in s_side (direct: now;
-    // staged: gathered after the descriptors, needed only after the flat pass)
-    int par = 0;  // iteration parity (s_nside / s_bad)
-    auto put_side = [&](uint32_t e, uint32_t c4, uint32_t j_or_0, uint64_t wv, bool have_w) {
-        const uint32_t k = atomicAdd(&s_nside[par], 1u);
-        if (k < (uint32_t)kLprSide) {
-            if (have_w) s_side[k] = wv;
-            s_sidej[k] = j_or_0;
-        } else {
-            s_bad[par] = 1;
-        }
-        s_desc[e] = 0xc0000000u | (c4 << 26) | k;
-    };
-    auto put_words = [&](uint32_t ne, uint32_t b0) {
-        if constexpr (STAGED) {
-#pragma unroll
-            for (int u = 0; u < kU; ++u)
-                if (b0 + tid + u * kLprRows < ne) {
-                    if ((dv[u] >> 30) == 3) put_side(sv[u] >> 20, (dv[u] >> 26) & 15u, dv[u] & kW32J, 0ull, false);
-                    else s_desc[sv[u] >> 20] = dv[u];  // the W32 word: same bits as W's slots 0-1
-                }
-        } else {
-            uint64_t wv[kU];
-#pragma unroll
-            for (int u = 0; u < kU; ++u) wv[u] = sv[u] != 0xffffffffu ? R.W[sv[u]] : 0ull;
-#pragma unroll
-            for (int u = 0; u < kU; ++u)
-                if (b0 + tid + u * kLprRows < ne) {
-                    const uint64_t x = wv[u];
-                    const uint32_t n = (uint32_t)(x >> 61);
-                    if (n <= 2) s_desc[b0 + tid + u * kLprRows] = (n << 30) | (uint32_t)(x & 0x3fffffffu);
-                    else put_side(b0 + tid + u * kLprRows, std::min(n != 7 ? n : (uint32_t)R.O[x & kLow61], 15u), 0u,
-                                  x, true);
-                }
-        }
-    };
-    auto go_heavy = [&](unsigned tile) {  // one lane of the tile: the heavy path takes the whole tile
-        if (atomicOr(&sp.tflag[tile], 1u) == 0u) sp.hlist[atomicAdd(&ws->n_deferred, 1u)] = tile;
-    };
-
-    if (stg.gate && *stg.gate == 0) return;  // uniform: the device chose direct gathers for this call
-    // ---- pipeline prologue: the first tile's two rounds
-    unsigned k = blockIdx.x;
-    Pre cur = round1(k);
-    if (cur.tile >= n_tiles) return;  // uniform: no tile for this workgroup
-    if (tid == 0) {
-        s_nside[0] = 0;
-        s_bad[0] = 0;
-    }
-    uint32_t cur_pre = stage_runs(cur);  // (its barriers also publish the resets above)
-    round2(cur, 0, cur_pre);
-    first_values(cur);
-    while (true) {
-        // ---- A: this tile's descriptors into LDS
-        const unsigned tile = cur.tile;
-        const int nrows = cur.nrows;
-        const int64_t ea = (int64_t)cur.a0;
-        const int64_t ne64 = (int64_t)cur.an - ea;
-        const uint32_t ne = (uint32_t)ne64;
-        const uint32_t E0 = (uint32_t)((int64_t)cur.ae0 - ea), E1 = (uint32_t)((int64_t)cur.ae1 - ea);
-        const int64_t rp0 = (int64_t)cur.arp0, rp1 = (int64_t)cur.arp1;
-        const T* __restrict__ Axw = Ax + ea;
-        T xv[kXP];
-#pragma unroll
-        for (int j = 0; j < kXP; ++j) xv[j] = xn[j];
-        const bool too_many = ne64 > cap_a;  // uniform
-        __syncthreads();  // previous tile done with s_desc / slots / side table / its flags
-        STAMP(0);
-        if (tid == 0) {  // the next tile's pair (its last readers were the tile before this one)
-            s_nside[par ^ 1] = 0;
-            s_bad[par ^ 1] = 0;
-        }
-        if (!too_many) {
-            put_words(ne, 0);
-            // the rest of a large tile, synchronously (rare); s_ksrc / s_sbm still hold its runs
-            for (uint32_t b0 = kU * kLprRows; b0 < ne; b0 += kU * kLprRows) {
-                round2(cur, b0, cur_pre);
-                put_words(ne, b0);
-            }
-        }
-        if (tid <= nrows) s_rowptr[tid] = (uint16_t)(rp0 - ea);
-        if (tid == 0 && nrows == kLprRows) s_rowptr[kLprRows] = (uint16_t)(rp1 - ea);
-        STAMP(1);
-        // ---- the next tile's round 1, in flight during this tile's flat pass
-        k += gridDim.x;
-        const Pre nxt = round1(k);
-        __syncthreads();
-        STAMP(2);
-        const bool skip = too_many || s_bad[par] != 0;  // uniform: too many entries or the side table is full
-        if (skip && tid == 0) go_heavy(tile);
-        // staged: the W words of the side entries are gathered now and only needed after the flat
-        // pass (their counts came with the staged words), so this latency hides behind the pass
-        const uint32_t nside = skip ? 0u : s_nside[par];
-        uint64_t sidew = 0;
-        if (STAGED && (uint32_t)tid < nside) sidew = R.W[s_sidej[tid]];
-        // ---- step B: one wave per 64 rows, one flat pass over the wave's entries
-        const int r = tid;  // this lane's row (for per-row work)
-        const bool valid = r < nrows;
-        const uint32_t rs = valid ? s_rowptr[r] : 0u, re = valid ? s_rowptr[r + 1] : 0u;
-        const uint32_t nsteps = skip ? 0u : (E1 - E0 + 63) >> 6;
-        for (uint32_t q = lane; q < nsteps; q += 64) s_flag[w][q] = 0ull;
-        if (lane == 0) s_susp[w] = 0ull;
-        __builtin_amdgcn_wave_barrier();
-        const bool nonempty = !skip && re > rs;
-        const uint64_t ne_mask = __ballot(nonempty);
-        if (nonempty) {
-            const uint32_t b = rs - E0;
-            atomicOr(reinterpret_cast<unsigned long long*>(&s_flag[w][b >> 6]), 1ull << (b & 63));
-            s_nz2row[w][__builtin_popcountll(ne_mask & ((1ull << lane) - 1))] = (uint8_t)lane;
-        }
-        __builtin_amdgcn_wave_barrier();
-        // the wave's slot is built in LDS (columns cb, values vb, first-touch order) and stored to
-        // HBM with coalesced stores at the end
-        uint16_t* cb = s_colbuf + (size_t)w * sp.slot;
-        T* vb = s_valbuf + (size_t)w * sp.slot;
-        uint32_t carry_r = 0, carry_k = 0;
-        const T nmag = -mag;
-        auto ldx = [&](uint32_t j) {
-            const uint32_t e = E0 + 64 * j + lane;
-            const uint32_t elast = E1 > E0 ? E1 - 1 : E0;
-            const T v = Axw[std::min(e, elast)];
-            return e < E1 ? v : T(0);
-        };
-        auto step = [&](uint32_t j, T x) {
-            const uint32_t e = E0 + 64 * j + lane;
-            const bool ve = e < E1;
-            const uint64_t fw = s_flag[w][j];
-            const uint32_t nr = carry_r + (uint32_t)__builtin_popcountll(fw & ((2ull << lane) - 1)) - 1u;
-            const uint32_t row = s_nz2row[w][nr & 63];
-            const uint32_t d = ve ? s_desc[e] : 0u;
-            const uint32_t n = d >> 30;
-            const uint32_t np = n < 3 ? n : (d >> 26) & 15u;  // n == 3: a side entry (count in the word)
-            const bool nzx = tmul<T>(x, mag) != T(0);  // all products of an entry share |x * mag|
-            const uint32_t kc = nzx ? np : 0u;
-            const uint32_t kinc = wave_scan_dpp(kc);
-            const uint32_t K = carry_k + kinc - kc;
-            if (ve && ((fw >> lane) & 1ull)) s_kst[w][row] = (uint16_t)K;  // the row's first entry
-            const uint32_t sl0 = d & 0x7fffu, sl1 = (d >> 15) & 0x7fffu;
-            if (n < 3 && kc >= 1 && K < sp.slot) {
-                cb[K] = (uint16_t)(sl0 & 0x3fffu);
-                vb[K] = tadd<T>(T(0), tmul<T>(x, (sl0 & 0x4000u) ? nmag : mag));
-            }
-            if (n < 3 && kc >= 2 && K + 1 < sp.slot) {
-                cb[K + 1] = (uint16_t)(sl1 & 0x3fffu);
-                vb[K + 1] = tadd<T>(T(0), tmul<T>(x, (sl1 & 0x4000u) ? nmag : mag));
-            }
-            // side entries keep a gap [K, K + np) in the slot, filled after the pass (their W words
-            // may still be in flight); a zero product is not in the slot: its row takes the exact path
-            if (n == 3) {
-                const uint32_t kk = d & kW32J;
-                s_sfk[kk] = kc ? (uint16_t)K : (uint16_t)0xffffu;
-                s_sfw[kk] = (uint8_t)w;
-                s_sfx[kk] = x;
-                if (np == 15) s_bad[par] = 1;  // 15 or more entries: the count is not exact -> heavy tile
-            }
-            if (ve && np > 0 && !nzx) atomicOr(reinterpret_cast<unsigned long long*>(&s_susp[w]), 1ull << row);
-            carry_k += __builtin_amdgcn_readlane(kinc, 63);
-            carry_r += (uint32_t)__builtin_popcountll(fw);
-        };
-        // values straight from HBM in entry order (coalesced), kXP steps in flight ahead of use, in
-        // two alternating register sets: no copy at the loop edge, so a step waits only for the
-        // loads issued a half-iteration earlier (a copy there made every iteration wait for the
-        // loads it had just issued)
-        for (uint32_t j = 0; j < nsteps; j += 2 * kXP) {
-            T xw[kXP];
-#pragma unroll
-            for (int u = 0; u < kXP; ++u) xw[u] = ldx(j + kXP + u);
-#pragma unroll
-            for (int u = 0; u < kXP; ++u)
-                if (j + u < nsteps) step(j + u, xv[u]);
-            if (j + kXP >= nsteps) break;  // uniform
-#pragma unroll
-            for (int u = 0; u < kXP; ++u) xv[u] = ldx(j + 2 * kXP + u);
-#pragma unroll
-            for (int u = 0; u < kXP; ++u)
-                if (j + kXP + u < nsteps) step(j + kXP + u, xw[u]);
-        }
-        bool overflow = carry_k > sp.slot;
-        STAMP(3);
-        __syncthreads();
-        // side fill: every side entry's products into its gap, in R's storage order
-        if ((uint32_t)tid < nside) {
-            const uint64_t sw = STAGED ? sidew : s_side[tid];
-            if (STAGED) s_side[tid] = sw;
-            const uint32_t k0 = s_sfk[tid];
-            if (k0 != 0xffffu) {
-                uint16_t* cbw = s_colbuf + (size_t)s_sfw[tid] * sp.slot;
-                T* vbw = s_valbuf + (size_t)s_sfw[tid] * sp.slot;
-                const T x = s_sfx[tid];
-                const bool rec = (sw >> 61) == 7;
-                const uint32_t np = rec ? R.O[sw & kLow61] : (uint32_t)(sw >> 61);
-                for (uint32_t t = 0; t < np && k0 + t < sp.slot; ++t) {
-                    uint32_t sl;
-                    if (rec) {
-                        const uint32_t e = R.O[(sw & kLow61) + 1 + t];
-                        sl = ((e & 0x8000u) >> 1) | (e & 0x3fffu);
-                    } else {
-                        sl = (uint32_t)(sw >> (15 * t)) & 0x7fffu;
-                    }
-                    cbw[k0 + t] = (uint16_t)(sl & 0x3fffu);
-                    vbw[k0 + t] = tadd<T>(T(0), tmul<T>(x, (sl & 0x4000u) ? -mag : mag));
-                }
-            }
-        }
-        // ---- the next tile's round 2, in flight during this tile's row phase. The run table's two
-        // barriers also publish the side fill (and s_bad) to the row phase
-        uint32_t npre = 0;
-        if (STAGED && nxt.tile < n_tiles) npre = stage_runs(nxt);
-        else __syncthreads();
-        const bool bad2 = s_bad[par] != 0;  // uniform: a side entry with 15 or more products
-        if (nxt.tile < n_tiles) {
-            round2(nxt, 0, npre);
-            first_values(nxt);
-        }
-        if (!skip && bad2 && tid == 0) go_heavy(tile);
-        STAMP(4);
-        if (!skip && !bad2) {
-            // ---- per row: kept count and a Bloom check of its columns (3 x 64-bit filters in
-            // registers): a column whose 3 bits are all set already flags the row for the exact
-            // path (every real repeat does; false alarms ~ (i/64)^3 for the i-th product)
-            const uint32_t kst = nonempty ? s_kst[w][lane] : 0u;
-            const uint64_t after = ne_mask & ~((2ull << lane) - 1);  // the next non-empty row ends this one
-            const int nx = after ? __builtin_ctzll(after) : 64;
-            const uint32_t kst_next = __shfl(kst, nx & 63, 64);
-            const uint32_t kend_r = nx < 64 ? kst_next : carry_k;
-            uint32_t kept = nonempty ? kend_r - kst : 0u;
-            bool hit = false;
-            if (!overflow) hit = lpr_bloom(cb, kst, kept);
-            uint64_t todo = s_susp[w] | __ballot(hit);  // lane == row within the wave
-            __builtin_amdgcn_wave_barrier();  // the row-start bitmap is dead from here: the scratch reuses it
-            constexpr int kScr = (int)((kLprFlagWords * 8 - 16) / (2 + sizeof(T)));
-            uint16_t* scol = reinterpret_cast<uint16_t*>(&s_flag[w][0]);
-            T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(&s_flag[w][0]) + ((2 * kScr + 15) & ~15));
-            if (__ballot(overflow)) todo = 0;
-            // exact path, one flagged row at a time, the whole wave on it: its products in sequence
-            // order into the scratch, then every product checks for an earlier one of its column
-            // (first touch); a leader sums its group in order; kept leaders land in the row's slot
-            // range in that order
-            while (todo) {
-                const int R0 = __builtin_ctzll(todo);
-                todo &= todo - 1;
-                const uint32_t a0 = __shfl(rs, R0, 64), a1 = __shfl(re, R0, 64), kR = __shfl(kst, R0, 64);
-                uint32_t nprod = 0;
-                for (uint32_t e0 = a0; e0 < a1; e0 += 64) {
-                    const uint32_t e = e0 + lane;
-                    const bool in = e < a1;
-                    const uint32_t d = in ? s_desc[e] : 0u;
-                    const T x = in ? Axw[e] : T(0);
-                    const uint32_t np = in ? ((d >> 30) < 3 ? (d >> 30) : (d >> 26) & 15u) : 0u;
-                    const uint32_t inc = wave_scan_dpp(np);
-                    const uint32_t q0 = nprod + inc - np;
-                    for (uint32_t t = 0; t < np; ++t)
-                        if (q0 + t < (uint32_t)kScr) {
-                            const uint32_t sl = lpr_slot(d, t, s_side, R.O);
-                            scol[q0 + t] = (uint16_t)(sl & 0x3fffu);
-                            sval[q0 + t] = tmul<T>(x, (sl & 0x4000u) ? -mag : mag);
-                        }
-                    nprod += __builtin_amdgcn_readlane(inc, 63);
-                }
-                if (nprod > (uint32_t)kScr) {
-                    overflow = true;
-                    break;
-                }
-                __builtin_amdgcn_wave_barrier();
-                uint32_t nk = 0;
-                for (uint32_t q0 = 0; q0 < nprod; q0 += 64) {
-                    const uint32_t q = q0 + lane;
-                    bool lead = q < nprod;
-                    T sum = T(0);
-                    if (lead) {
-                        const uint16_t cq = scol[q];
-                        for (uint32_t b = 0; b < q && lead; ++b) lead = scol[b] != cq;
-                        if (lead) {
-                            sum = tadd<T>(T(0), sval[q]);
-                            for (uint32_t b = q + 1; b < nprod; ++b)
-                                if (scol[b] == cq) sum = tadd<T>(sum, sval[b]);
-                        }
-                    }
-                    const bool keep = lead && sum != T(0);
-                    const uint32_t ki = wave_scan_dpp(keep ? 1u : 0u);
-                    if (keep) {
-                        if (kR + nk + ki - 1 >= sp.slot) overflow = true;
-                        else {
-                            cb[kR + nk + ki - 1] = scol[q];
-                            vb[kR + nk + ki - 1] = sum;
-                        }
-                    }
-                    nk += __builtin_amdgcn_readlane(ki, 63);
-                }
-                if (lane == R0) kept = nk;
-                __builtin_amdgcn_wave_barrier();
-            }
-            // a row that gained entries in the exact path (its side entries were not in the slot)
-            // must still end before the next row's range
-            if (kst + kept > kend_r && nonempty) overflow = true;
-            if (__ballot(overflow)) {  // this wave cannot finish on the fast path: the whole tile goes heavy
-                if (lane == 0) go_heavy(tile);
-            } else {
-                if (order == RP_ORDER_SORTED && kept > 1) {  // ascending columns inside the row's slot range
-                    for (uint32_t a = kst + 1; a < kst + kept; ++a) {
-                        const uint16_t kc = cb[a];
-                        const T kv = vb[a];
-                        uint32_t b = a;
-                        while (b > kst && cb[b - 1] > kc) {
-                            cb[b] = cb[b - 1];
-                            vb[b] = vb[b - 1];
-                            --b;
-                        }
-                        cb[b] = kc;
-                        vb[b] = kv;
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-                const size_t wt = (size_t)tile * 4 + w;
-                lpr_store_rows<T>(cb, vb, kst, kept, valid, lane, order, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
-                                  sp.cnt + wt, sp.cols + wt * sp.slot, reinterpret_cast<T*>(sp.vals) + wt * sp.slot);
-            }
-        }
-        STAMP(5);
-        STAMP(6);
-        if (nxt.tile >= n_tiles) break;  // uniform
-        cur = nxt;
-        cur_pre = npre;
-        par ^= 1;
-    }
-}
-
 // One workgroup per tile, no persistence (direct gathers: the two dependent rounds, feature ids
 // then W words, are cheaper to hide with more resident tiles than with cross-tile pipelining;
-// measured: power-law direct main kernel 12.4 ms here vs 15.3 ms persistent)
-template <typename T, typename IP, bool STAGED>
+// measured: power-law direct main kernel 12.4 ms here vs 15.3 ms persistent). Launched when the
+// call takes direct gathers (the host read lpr_choose_kernel's verdict, or staging is off).
+template <typename T, typename IP>
 __global__ void __launch_bounds__(kLprRows)
 lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
-                const T* __restrict__ Ax, LprStage stg, int cap_a, unsigned n_tiles, unsigned t8, int order,
-                LprSpace sp, Workspace* ws) {
-    if (!STAGED && stg.gate && *stg.gate != 0) return;  // uniform: the device chose the staged gather
+                const T* __restrict__ Ax, const uint32_t* __restrict__ w32, int cap_a, unsigned n_tiles, unsigned t8,
+                int order, LprSpace sp, Workspace* ws) {
     extern __shared__ __align__(16) unsigned char lds[];          // s_desc[cap_a] u32
     __shared__ uint16_t s_rowptr[kLprRows + 1];
     __shared__ uint64_t s_side[kLprSide];
-    __shared__ uint32_t s_sidej[kLprSide];                          // side entry's feature (staged)
+    __shared__ uint32_t s_sidej[kLprSide];                          // side entry's SW index (W32 gathers)
     __shared__ uint16_t s_sfk[kLprSide];                            // side entry's slot position
     __shared__ uint8_t s_sfw[kLprSide];                             // ... in the slot of this wave
     __shared__ T s_sfx[kLprSide];                                   // ... and its value
@@ -1907,7 +1266,7 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     __shared__ uint64_t s_susp[4];                                  // rows flagged for the exact path
     __shared__ uint16_t s_kst[4][64];
     __shared__ uint8_t s_nz2row[4][64];
-    __shared__ uint32_t s_nside, s_scr[4], s_wnz[4];
+    __shared__ uint32_t s_nside, s_scr[4];
     __shared__ int s_bad;
     uint32_t* s_desc = reinterpret_cast<uint32_t*>(lds);
     uint16_t* s_colbuf = reinterpret_cast<uint16_t*>(lds + ((4 * (size_t)cap_a + 15) & ~size_t(15)));  // 4 x slot
@@ -1932,29 +1291,6 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
         s_bad = ne64 > cap_a;
     }
     if (tid < 4) s_scr[tid] = 0;
-    // staged: the tile's run table, loaded together with the row pointers. Run b holds the entries
-    // q in [st_b, st_b + len_b) (bucket order) at S/D index src_b + q - st_b, relative to the
-    // group's first segment. Element -> run: bit q of s_sbm marks the start of a nonempty run, so
-    // the k-th nonempty run holds q for k = (set bits at or below q) - 1, and s_ksrc[k] gives its
-    // index offset. Both live in the slot buffers, which the flat pass fills only later.
-    uint32_t* s_ksrc = reinterpret_cast<uint32_t*>(s_colbuf);
-    uint64_t* s_sbm = reinterpret_cast<uint64_t*>(s_colbuf + 2 * kStageMaxNB);
-    uint32_t m_st = 0, m_len = 0, m_src = 0;
-    uint64_t nzb = 0;
-    int64_t g0 = 0;
-    if constexpr (STAGED) {
-        const size_t gb = (size_t)(tile / kRunGroup) * stg.nb;
-        g0 = stg.gb[gb];
-        if (tid < stg.nb) {
-            const size_t o = (size_t)tile * stg.ostride + tid;
-            m_st = stg.offt[o];
-            m_len = stg.offt[o + 1] - m_st;
-            m_src = (uint32_t)(stg.gb[gb + tid] - g0) + stg.off2[o];
-        }
-        if (tid < 64) s_sbm[tid] = 0ull;
-        nzb = __ballot(m_len > 0);
-        if ((tid & 63) == 0) s_wnz[tid >> 6] = (uint32_t)__popcll(nzb);
-    }
     __syncthreads();
     auto go_heavy = [&]() {  // one lane of the tile: the heavy path takes the whole tile
         if (atomicOr(&sp.tflag[tile], 1u) == 0u) sp.hlist[atomicAdd(&ws->n_deferred, 1u)] = tile;
@@ -1963,7 +1299,6 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
         if (tid == 0) go_heavy();
         return;
     }
-    STAMP(0);
     const uint32_t ne = (uint32_t)ne64;
     // the flat pass's first values (entry order, coalesced) in flight together with step A's loads;
     // unconditional loads (index clamped, value masked): straight-line vmcnt accounting
@@ -1978,7 +1313,8 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     // ---- step A: R descriptors of the tile's entries into LDS, by entry
     // LDS descriptor of an entry: n <= 2 -> the W32 form (count, two inline 15-bit slots);
     // more entries -> code 3 | count (4 bits) << 26 | side index: the feature's W word lands in
-    // s_side[k] (direct: now; staged: gathered after step A, needed only after the flat pass)
+    // s_side[k] (8-byte W gathers: now; W32 gathers: from SW after step A, needed only after the
+    // flat pass)
     auto put_side = [&](uint32_t e, uint32_t c4, uint32_t j_or_0, uint64_t w, bool have_w) {
         const uint32_t k = atomicAdd(&s_nside, 1u);
         if (k < (uint32_t)kLprSide) {
@@ -1995,41 +1331,7 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
         else put_side(e, std::min(n != 7 ? n : (uint32_t)R.O[w & kLow61], 15u), 0u, w, true);
     };
     constexpr int kU = 12;  // loads of a round issued before any is used
-    if constexpr (STAGED) {
-        const int ln = tid & 63, wv = tid >> 6;
-        if (m_len > 0) {
-            uint32_t k = (uint32_t)__popcll(nzb & ((1ull << ln) - 1ull));
-            for (int i = 0; i < wv; ++i) k += s_wnz[i];
-            s_ksrc[k] = m_src - m_st;
-            atomicOr(&s_sbm[m_st >> 6], 1ull << (m_st & 63));
-        }
-        __syncthreads();
-        const uint32_t c = (uint32_t)__popcll(s_sbm[ln]);
-        const uint32_t pre = wave_scan_dpp(c) - c;  // set bits in the words below word ln
-        const uint32_t* __restrict__ St = stg.s + g0;
-        const uint32_t* __restrict__ Dt = stg.d + g0;
-        // block-uniform trip count: every lane of a wave takes part in the shuffle (a lane that had
-        // left the loop would hand back an undefined `pre` to the lanes still in it)
-        for (uint32_t b0 = 0; b0 < ne; b0 += kU * kLprRows) {
-            const uint32_t q0 = b0 + tid;
-            uint32_t sv[kU], dv[kU];
-#pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const uint32_t q = std::min(q0 + u * kLprRows, ne - 1);
-                const uint32_t k = (uint32_t)__shfl((int)pre, (int)(q >> 6), 64) +
-                                   (uint32_t)__popcll(s_sbm[q >> 6] & (~0ull >> (63 - (q & 63)))) - 1u;
-                const uint32_t i = s_ksrc[k] + q;
-                sv[u] = q0 + u * kLprRows < ne ? St[i] : 0u;
-                dv[u] = q0 + u * kLprRows < ne ? Dt[i] : 0u;
-            }
-#pragma unroll
-            for (int u = 0; u < kU; ++u)
-                if (q0 + u * kLprRows < ne) {
-                    if ((dv[u] >> 30) == 3) put_side(sv[u] >> 20, (dv[u] >> 26) & 15u, dv[u] & kW32J, 0ull, false);
-                    else s_desc[sv[u] >> 20] = dv[u];  // the W32 word: same bits as W's slots 0-1
-                }
-        }
-    } else {
+    {
         const int32_t* __restrict__ Ajt = Aj + ea;
         for (uint32_t q0 = tid; q0 < ne; q0 += kU * kLprRows) {
             int32_t jv[kU];
@@ -2038,10 +1340,10 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
                 const uint32_t e = q0 + u * kLprRows;
                 jv[u] = e < ne ? Ajt[e] : -1;
             }
-            if (stg.w32) {  // the 4-byte W32 words: twice the features per line; > 2 entries -> side
+            if (w32) {  // the 4-byte W32 words: twice the features per line; > 2 entries -> side
                 uint32_t w[kU];
 #pragma unroll
-                for (int u = 0; u < kU; ++u) w[u] = jv[u] >= 0 ? stg.w32[jv[u]] : 0u;
+                for (int u = 0; u < kU; ++u) w[u] = jv[u] >= 0 ? w32[jv[u]] : 0u;
 #pragma unroll
                 for (int u = 0; u < kU; ++u)
                     if (q0 + u * kLprRows < ne) {
@@ -2060,19 +1362,17 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     }
     if (tid <= nrows) s_rowptr[tid] = (uint16_t)(rp0 - ea);
     if (tid == 0 && nrows == kLprRows) s_rowptr[kLprRows] = (uint16_t)(rp1 - ea);
-    STAMP(1);
     __syncthreads();
-    STAMP(2);
     if (s_bad) {  // uniform: side table full
         if (tid == 0) go_heavy();
         return;
     }
-    // staged: the W words of the side entries are gathered now and only needed after the flat
-    // pass (their counts came with the staged words), so this latency hides behind the pass
+    // W32 gathers: the W words of the side entries are gathered now (from the side table) and
+    // only needed after the flat pass (their counts came with the W32 words)
     const uint32_t nside = s_nside;
     uint64_t sidew = 0;
-    const bool side_later = STAGED || stg.w32 != nullptr;  // side W words not in LDS yet
-    if (side_later && (uint32_t)tid < nside) sidew = R.W[s_sidej[tid]];
+    const bool side_later = w32 != nullptr;  // side W words not in LDS yet
+    if (side_later && (uint32_t)tid < nside) sidew = R.SW[s_sidej[tid]];
     // ---- step B: one wave per 64 rows, one flat pass over the wave's entries
     const int w = tid >> 6, lane = tid & 63;
     const int r = tid;  // this lane's row (for per-row work)
@@ -2182,7 +1482,6 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
         if (tid == 0) go_heavy();
         return;
     }
-    STAMP(3);
     // ---- per row: kept count and a Bloom check of its columns (3 x 64-bit filters in registers):
     // a column whose 3 bits are all set already flags the row for the exact path (every real
     // repeat does; false alarms ~ (i/64)^3 for the i-th product)
@@ -2282,151 +1581,89 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     const size_t wt = (size_t)tile * 4 + w;
     lpr_store_rows<T>(cb, vb, kst, kept, valid, lane, order, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
                       sp.cnt + wt, sp.cols + wt * sp.slot, reinterpret_cast<T*>(sp.vals) + wt * sp.slot);
-    STAMP(4);
-    STAMP(5);
-    STAMP(6);
 }
 
 // ------------------------------------------------------------------------------------------
-// Split row-lane pipeline, the staged default: the main kernel's two halves as
-// two launches, so that the compute half runs without block barriers at full occupancy.
-//   lpr_unsort_kernel (M1)  staged descriptors back into entry order (DE, tile-strided)
-//   lpr_wave_kernel   (M2)  one wave per 64 rows, independent of every other wave
-// Measured reason: the persistent main kernel is latency-bound (64% of wave cycles
-// waiting at 4 waves per SIMD, six block barriers per tile) and insensitive to its fetch volume
-// (twice longer staged runs: -2%).
-
-// M1: one workgroup per super-tile (one 256-thread quarter per tile, kPartTiles tiles): the tile's
-// run table (OFFT / OFF2 / GB) -> element -> run lookup (start bitmap + popcount), the S/D words of
-// its runs (the super-tile's runs of a bucket are adjacent, so the four quarters' loads of a bucket
-// cover one contiguous range), each D word scattered by S's entry index into LDS, then the tile's
-// descriptors stored in entry order at DE[tile * cap_a + e], coalesced. A descriptor is the W32
-// word (n <= 2 entries inline; code 3 = more: count << 26 | feature). Heavy tiles (more than cap_a
-// entries) staged nothing and are skipped.
-template <typename IP>
-__global__ void __launch_bounds__(kPBlock)
-lpr_unsort_kernel(const IP* __restrict__ Ap, int64_t n_rows, LprStage stg, int cap_a, unsigned n_tiles, unsigned s8,
-                  uint32_t* __restrict__ DE) {
-    extern __shared__ __align__(16) uint32_t s_desc[];  // [kPartTiles][cap_a]
-    __shared__ uint32_t s_ksrc[kPartTiles][kStageMaxNB];
-    __shared__ uint64_t s_sbm[kPartTiles][64];
-    __shared__ uint32_t s_wnz[kPBlock / 64];
-    if (*stg.gate == 0) return;  // uniform (written only by earlier launches)
-    const int tid = threadIdx.x, q = tid >> 8, qt = tid & (kBlock - 1), w = tid >> 6, lane = tid & 63;
-    const unsigned t0 = xcd_tile(blockIdx.x, s8) * kPartTiles;
-    if (t0 >= n_tiles) return;  // uniform
-    const unsigned t = t0 + q;
-    int64_t ea = 0, ne = 0;
-    if (t < n_tiles) {
-        const int64_t row0 = (int64_t)t * kLprRows;
-        ea = (int64_t)Ap[row0];
-        ne = (int64_t)Ap[std::min<int64_t>(row0 + kLprRows, n_rows)] - ea;
-    }
-    const uint32_t n = ne <= cap_a ? (uint32_t)ne : 0u;  // quarter-uniform
-    uint32_t m_st = 0, m_len = 0, m_src = 0;
-    int64_t g0 = 0;
-    if (n > 0) {
-        const size_t gb = (size_t)(t / kRunGroup) * stg.nb;
-        g0 = stg.gb[gb];
-        if (qt < stg.nb) {
-            const size_t o = (size_t)t * stg.ostride + qt;
-            m_st = stg.offt[o];
-            m_len = stg.offt[o + 1] - m_st;
-            m_src = (uint32_t)(stg.gb[gb + qt] - g0) + stg.off2[o];
-        }
-    }
-    if (qt < 64) s_sbm[q][qt] = 0ull;
-    const uint64_t nzb = __ballot(m_len > 0);
-    if (lane == 0) s_wnz[w] = (uint32_t)__popcll(nzb);
-    __syncthreads();
-    // run k of the tile (k-th nonempty bucket) starts at element st: bit st of the start bitmap,
-    // its words at S/D index s_ksrc[k] + element (relative to the group's first segment)
-    if (m_len > 0) {
-        uint32_t k = (uint32_t)__popcll(nzb & ((1ull << lane) - 1ull));
-        for (int i = 4 * q; i < w; ++i) k += s_wnz[i];
-        s_ksrc[q][k] = m_src - m_st;
-        atomicOr(reinterpret_cast<unsigned long long*>(&s_sbm[q][m_st >> 6]), 1ull << (m_st & 63));
-    }
-    __syncthreads();
-    const uint32_t c = (uint32_t)__popcll(s_sbm[q][lane]);
-    const uint32_t pre = wave_scan_dpp(c) - c;  // set bits in the words below word `lane`
-    const uint32_t* __restrict__ St = stg.s + g0;
-    const uint32_t* __restrict__ Dt = stg.d + g0;
-    uint32_t* sd = s_desc + (size_t)q * cap_a;
-    constexpr int kU = 12;
-    // quarter-uniform trip count: every lane of a wave takes part in the shuffle
-    for (uint32_t b0 = 0; b0 < n; b0 += kU * kBlock) {
-        const uint32_t q0 = b0 + qt;
-        uint32_t sv[kU], dv[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-            const uint32_t e = std::min(q0 + u * kBlock, n - 1);
-            const uint32_t k = (uint32_t)__shfl((int)pre, (int)(e >> 6), 64) +
-                               (uint32_t)__popcll(s_sbm[q][e >> 6] & (~0ull >> (63 - (e & 63)))) - 1u;
-            const uint32_t i = s_ksrc[q][k] + e;
-            sv[u] = q0 + u * kBlock < n ? __builtin_nontemporal_load(St + i) : 0u;
-            dv[u] = q0 + u * kBlock < n ? __builtin_nontemporal_load(Dt + i) : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kU; ++u)
-            if (q0 + u * kBlock < n) sd[sv[u] >> 20] = dv[u];
-    }
-    __syncthreads();
-    uint32_t* __restrict__ DEt = DE + (size_t)t * cap_a;
-    for (uint32_t e = qt; e < n; e += kBlock) DEt[e] = sd[e];
-}
-
-// t-th product's (sign << 14 | col) of an entry with DE descriptor d (code 3: W[feature])
-__device__ __forceinline__ uint32_t lpr_slot_de(uint32_t d, uint32_t t, const uint64_t* W, const uint16_t* O) {
-    if ((d >> 30) < 3) return (d >> (15 * t)) & 0x7fffu;
-    const uint64_t w = W[d & kW32J];
-    if ((w >> 61) != 7) return (uint32_t)(w >> (15 * t)) & 0x7fffu;
-    const uint32_t e = O[(w & kLow61) + 1 + t];
-    return ((e & 0x8000u) >> 1) | (e & 0x3fffu);
-}
-
-// M2: one 64-thread workgroup = one wave = one 64-row unit (tile rb / 4, wave rb % 4 of the
-// workspace layout the scan / copy / heavy kernels read). Round 1: the unit's row pointers (and
-// its tile's entry count: a heavy tile goes to the exact path whole). Round 2: descriptors and
-// values of up to kWaveSteps x 64 entries, coalesced, all in flight together. The flat pass then
+// Staged row-lane wave kernel, the uniform-column default: one 64-thread
+// workgroup = one wave = one 64-row unit, independent of every other wave (no block barrier, full
+// occupancy). Round 1: the unit's row pointers and its part of the tile's run table (per bucket:
+// OFF2 + the unit's cumulative counts CU). Round 2: the S and D words of its parts of the runs
+// (bucket order; a super-tile's units read neighbouring parts of the same lines on one XCD) and
+// its values, all in flight together; each D word is put back in entry order by its S word's entry
+// index (LDS), then every lane holds its entries' descriptors in registers. The flat pass then
 // runs from registers: per step, an entry's row from the row-start bitmap, its products' kept
 // prefix (DPP scan) = their place in the slot, in first-touch order. Side entries (> 2 R entries)
-// keep a gap, filled after the pass from their W words (gathered once the pass has listed them).
-// The row phase is lpr_main_kernel's: Bloom check, exact path for flagged rows, optional sort,
-// row metadata, the slot stored coalesced.
-constexpr int kWaveSteps = 12;                 // flat-pass steps per load round (avg KDD2012: 11)
-constexpr int kWaveMaxSteps = 32;              // entries per unit beyond 32 x 64 -> heavy tile
+// keep a gap, filled after the pass from their side-table words. Row phase: Bloom check, exact
+// path for flagged rows, optional sort, row metadata, the slot stored coalesced.
+// A call whose partition overflowed a segment's reserve (gate 0) runs this kernel with direct
+// gathers: the unit's feature ids, then their W32 words.
+// (Round 4 ran an unsort kernel between the gather and this kernel: every descriptor written back
+// to HBM in entry order and read again, 10.6 GB per configs[1] pass)
+constexpr int kWaveSteps = 16;                 // entries per unit on the fast path: 16 x 64 (KDD2012: 704)
 // side entries (features with > 2 R entries, 1.9% of KDD2012's) per unit beyond this -> heavy tile.
 // Poisson tails: a 704-entry unit has 13.3 on average; 32 was exceeded by ~7 of 1.87M units per
 // configs[1] pass (4e-6 each), and 6 heavy tiles cost 1.6 ms; past 64: ~1e-24.
 constexpr int kWaveSide = 64;
 constexpr int kWaveScr = 128;                  // exact-path scratch (products of one row)
-__host__ __device__ inline size_t lpr_wave_lds_bytes(uint32_t slot, size_t vs) {
-    return ((2 * (size_t)slot + 15) & ~size_t(15)) + ((vs * (size_t)slot + 15) & ~size_t(15)) +
-           ((2 * (size_t)kWaveScr + 15) & ~size_t(15)) + vs * kWaveScr;
+// dynamic LDS: region A = the unit's descriptors (ucap words, entry order), later the slot's
+// columns + values (every descriptor is in registers before the first slot store); region B = the
+// run lookup (start bitmap, run offsets), later the exact-path scratch
+__host__ __device__ inline size_t lpr_wave_region_a(uint32_t slot, size_t vs, uint32_t ucap) {
+    const size_t s = ((2 * (size_t)slot + 15) & ~size_t(15)) + ((vs * (size_t)slot + 15) & ~size_t(15));
+    return std::max(s, 4 * (size_t)ucap);
 }
-template <typename T, typename IP>
-__global__ void __launch_bounds__(64)
-lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const T* __restrict__ Ax,
-                const uint32_t* __restrict__ DE, const uint32_t* __restrict__ gate, int cap_a, unsigned n_tiles,
+__host__ __device__ inline size_t lpr_wave_lds_bytes(uint32_t slot, size_t vs, uint32_t ucap, int nb) {
+    const size_t scr = ((2 * (size_t)kWaveScr + 15) & ~size_t(15)) + vs * kWaveScr;
+    const size_t tab = 8 * (size_t)kWaveSteps + 4 * (size_t)std::max(nb, 1);
+    return lpr_wave_region_a(slot, vs, ucap) + std::max(scr, tab);
+}
+// t-th product's (sign << 14 | col) of an entry with descriptor d (code 3: side-table word)
+__device__ __forceinline__ uint32_t lpr_slot_sw(uint32_t d, uint32_t t, const uint64_t* SW, const uint16_t* O) {
+    if ((d >> 30) < 3) return (d >> (15 * t)) & 0x7fffu;
+    const uint64_t w = SW[d & kW32J];
+    if ((w >> 61) != 7) return (uint32_t)(w >> (15 * t)) & 0x7fffu;
+    const uint32_t e = O[(w & kLow61) + 1 + t];
+    return ((e & 0x8000u) >> 1) | (e & 0x3fffu);
+}
+// v[x] for a runtime x (unrolled selects: no dynamic register indexing, no scratch; the empty asm
+// keeps the compiler from folding the selects back into an indexed load of a stack copy)
+template <int N>
+__device__ __forceinline__ uint32_t reg_pick(const uint32_t (&v)[N], uint32_t x) {
+    uint32_t r = v[0];
+#pragma unroll
+    for (int i = 1; i < N; ++i) {
+        uint32_t t = v[i];
+        __asm__("" : "+v"(t));
+        r = (uint32_t)i == x ? t : r;
+    }
+    return r;
+}
+// f32: built for 8 waves per SIMD (64 VGPRs; SGPRs were the limit at 7); f64 unconstrained
+template <typename T, typename IP, int WPE = std::is_same<T, float>::value ? 8 : 1>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
+lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                const T* __restrict__ Ax, LprStage stg, int cap_a, uint32_t ucap, unsigned n_tiles, unsigned s8,
                 int order, LprSpace sp, Workspace* ws) {
-    extern __shared__ __align__(16) unsigned char lds[];  // slot columns, slot values, exact-path scratch
-    __shared__ uint64_t s_flag[kWaveMaxSteps];            // row-start bitmap over the unit's entries
+    extern __shared__ __align__(16) unsigned char lds[];  // region A (descriptors, then slot), region B
+    __shared__ uint64_t s_flag[kWaveSteps];               // row-start bitmap over the unit's entries
     __shared__ uint64_t s_susp;                           // rows flagged for the exact path
     __shared__ uint16_t s_kst[64];
     __shared__ uint8_t s_nz2row[64];
     __shared__ uint16_t s_sfk[kWaveSide];                 // side entry's slot position (0xffff: zero x)
     __shared__ T s_sfx[kWaveSide];                        // ... its value
-    __shared__ uint32_t s_sfj[kWaveSide];                 // ... its feature
-    if (*gate == 0) return;  // uniform: the device chose direct gathers for this call
-    const unsigned rb = blockIdx.x, tile = rb >> 2;  // unit rb = wave rb % 4 of tile rb / 4
+    __shared__ uint32_t s_sfj[kWaveSide];                 // ... its side-table index
+    // unit order follows the partition's XCD ranges: XCD x takes the units of super-tiles
+    // [x * s8, (x + 1) * s8) in order (workgroup i runs on XCD i % 8)
+    const unsigned rb = (blockIdx.x & 7u) * (4u * kPartTiles * s8) + (blockIdx.x >> 3);
+    if (rb >= 4 * n_tiles) return;
+    const unsigned tile = rb >> 2, u = rb & 3;
     const int lane = threadIdx.x;
     const int64_t row0 = (int64_t)rb * 64;
-    if (tile >= n_tiles) return;
     if (row0 >= n_rows) {  // the last tile's empty units
         if (lane == 0) sp.cnt[rb] = 0u;
         return;
     }
+    const uint32_t staged = *stg.gate;  // uniform: 0 after a segment overflow (direct gathers)
     const int nrows = (int)std::min<int64_t>(64, n_rows - row0);
     const int64_t trow0 = (int64_t)tile * kLprRows;
     const int64_t ta = (int64_t)Ap[trow0];
@@ -2436,37 +1673,118 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     auto go_heavy = [&]() {  // the heavy path takes the whole tile (idempotent over its four units)
         if (lane == 0 && atomicOr(&sp.tflag[tile], 1u) == 0u) sp.hlist[atomicAdd(&ws->n_deferred, 1u)] = tile;
     };
-    const uint32_t nsteps = (E1 - E0 + 63) >> 6;
-    if (tn > cap_a || nsteps > (uint32_t)kWaveMaxSteps) {  // uniform: M1 staged nothing / too many
+    const uint32_t nu = E1 - E0, nsteps = (nu + 63) >> 6;
+    if (tn > cap_a || nu > ucap) {  // uniform: the partition staged nothing / too many for the registers
         go_heavy();
         return;
     }
-    const uint32_t* __restrict__ DEt = DE + (size_t)tile * cap_a;
     const T* __restrict__ Axt = Ax + ta;
+    const uint32_t elast = nu > 0 ? E1 - 1 : E0;
     uint32_t dv[kWaveSteps];
     T xv[kWaveSteps];
-    auto load_round = [&](uint32_t j0) {
+    uint32_t* desc = reinterpret_cast<uint32_t*>(lds);
+    const size_t ra = lpr_wave_region_a(sp.slot, sizeof(T), ucap);
+    if (staged) {
+        // this unit's part of tile run b: [c0, c1) of the run at GB[g, b] + OFF2[tile, b]
+        const size_t gq = (size_t)(tile / kRunGroup) * stg.nb;
+        const int64_t g0 = stg.gb[gq];
+        const uint16_t* __restrict__ cu = stg.cu + (size_t)tile * 4 * stg.ostride;
+        constexpr int kNBL = kStageMaxNB / 64;
+        uint32_t cnt[kNBL], src[kNBL];
 #pragma unroll
-        for (int u = 0; u < kWaveSteps; ++u) {
-            const uint32_t e = E0 + 64 * (j0 + u) + lane;
-            const uint32_t ec = std::min(e, E1 > E0 ? E1 - 1 : E0);
-            const uint32_t d = DEt[ec];
-            const T x = Axt[ec];
-            dv[u] = e < E1 ? d : 0u;
-            xv[u] = e < E1 ? x : T(0);
+        for (int h = 0; h < kNBL; ++h) {
+            const int b = 64 * h + lane;
+            cnt[h] = 0u;
+            src[h] = 0u;
+            if (b < stg.nb) {
+                const uint32_t c1 = cu[(size_t)u * stg.ostride + b];
+                const uint32_t c0 = u ? cu[(size_t)(u - 1) * stg.ostride + b] : 0u;
+                cnt[h] = c1 - c0;
+                src[h] = (uint32_t)(stg.gb[gq + b] - g0) + stg.off2[(size_t)tile * stg.ostride + b] + c0;
+            }
         }
-    };
-    if (nsteps > 0) load_round(0);  // (an empty unit loads nothing: E0 may be the array's end)
+        // the unit's layout: runs in bucket order; run k (k-th nonempty bucket) starts at layout
+        // position pos (bit pos of the start bitmap), its words at S/D index ksrc[k] + position
+        uint64_t* sbm = reinterpret_cast<uint64_t*>(lds + ra);
+        uint32_t* ksrc = reinterpret_cast<uint32_t*>(lds + ra + 8 * kWaveSteps);
+        if (lane < kWaveSteps) sbm[lane] = 0ull;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t pos0 = 0, nrun = 0;
+        const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+        for (int h = 0; h < kNBL; ++h) {
+            if (64 * h >= stg.nb) continue;  // uniform
+            const uint32_t inc = wave_scan_dpp(cnt[h]);
+            const uint32_t pos = pos0 + inc - cnt[h];
+            const uint64_t nz = __ballot(cnt[h] > 0);
+            if (cnt[h] > 0) {
+                ksrc[nrun + (uint32_t)__popcll(nz & lt)] = src[h] - pos;
+                atomicOr(reinterpret_cast<unsigned long long*>(&sbm[pos >> 6]), 1ull << (pos & 63));
+            }
+            pos0 += __builtin_amdgcn_readlane(inc, 63);
+            nrun += (uint32_t)__popcll(nz);
+        }
+        if (pos0 != nu) {  // uniform; cannot happen (the partition counted this tile): exact path
+            go_heavy();
+            return;
+        }
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t bc = lane < kWaveSteps ? (uint32_t)__popcll(sbm[lane]) : 0u;
+        const uint32_t bpre = wave_scan_dpp(bc) - bc;  // start bits in the bitmap words below `lane`
+        const uint32_t* __restrict__ St = stg.s + g0;
+        const uint32_t* __restrict__ Dt = stg.d + g0;
+        uint32_t sv[kWaveSteps];
+#pragma unroll
+        for (int x = 0; x < kWaveSteps; ++x) {
+            sv[x] = 0u;
+            dv[x] = 0u;
+            if ((uint32_t)x < nsteps) {  // uniform
+                const uint32_t p = std::min(64u * x + lane, nu - 1);
+                const uint32_t k = (uint32_t)__shfl((int)bpre, (int)(p >> 6), 64) +
+                                   (uint32_t)__popcll(sbm[p >> 6] & (~0ull >> (63 - (p & 63)))) - 1u;
+                const uint32_t i = ksrc[k] + p;
+                sv[x] = __builtin_nontemporal_load(St + i);
+                dv[x] = __builtin_nontemporal_load(Dt + i);
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < kWaveSteps; ++x)
+            if ((uint32_t)x < nsteps && 64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
+#pragma unroll
+        for (int x = 0; x < kWaveSteps; ++x) {  // the values: needed only by the flat pass
+            const uint32_t e = E0 + 64 * x + lane;
+            const T v = Axt[std::min(e, elast)];
+            xv[x] = e < E1 ? v : T(0);
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int x = 0; x < kWaveSteps; ++x) dv[x] = (uint32_t)x < nsteps && 64u * x + lane < nu ? desc[64 * x + lane] : 0u;
+        // every descriptor is in registers before the slot (region A) is written below
+        __builtin_amdgcn_wave_barrier();
+        __asm__ volatile("" ::: "memory");
+    } else {
+        const int32_t* __restrict__ Ajt = Aj + ta;
+        int32_t jv[kWaveSteps];
+#pragma unroll
+        for (int x = 0; x < kWaveSteps; ++x) {
+            const uint32_t e = E0 + 64 * x + lane;
+            const int32_t j = Ajt[std::min(e, elast)];
+            const T v = Axt[std::min(e, elast)];
+            jv[x] = e < E1 ? j : -1;
+            xv[x] = e < E1 ? v : T(0);
+        }
+#pragma unroll
+        for (int x = 0; x < kWaveSteps; ++x) dv[x] = jv[x] >= 0 ? stg.w32[jv[x]] : 0u;
+    }
     const uint32_t re = __shfl_down(rs, 1, 64);
     const uint32_t rend = lane == nrows - 1 ? E1 : (lane < nrows ? re : E1);
     const bool valid = lane < nrows;
     const bool nonempty = valid && rend > rs;
     uint16_t* cb = reinterpret_cast<uint16_t*>(lds);
     T* vb = reinterpret_cast<T*>(lds + ((2 * (size_t)sp.slot + 15) & ~size_t(15)));
-    uint16_t* scol = reinterpret_cast<uint16_t*>(lds + ((2 * (size_t)sp.slot + 15) & ~size_t(15)) +
-                                                 ((sizeof(T) * (size_t)sp.slot + 15) & ~size_t(15)));
-    T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(scol) + ((2 * (size_t)kWaveScr + 15) & ~size_t(15)));
-    for (uint32_t k = lane; k < nsteps; k += 64) s_flag[k] = 0ull;
+    uint16_t* scol = reinterpret_cast<uint16_t*>(lds + ra);
+    T* sval = reinterpret_cast<T*>(lds + ra + ((2 * (size_t)kWaveScr + 15) & ~size_t(15)));
+    if ((uint32_t)lane < nsteps) s_flag[lane] = 0ull;
     if (lane == 0) s_susp = 0ull;
     __builtin_amdgcn_wave_barrier();
     const uint64_t ne_mask = __ballot(nonempty);
@@ -2519,17 +1837,14 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         carry_k += __builtin_amdgcn_readlane(kinc, 63);
         carry_r += (uint32_t)__builtin_popcountll(fw);
     };
-    for (uint32_t j0 = 0; j0 < nsteps; j0 += kWaveSteps) {
-        if (j0 > 0) load_round(j0);  // rare: more than kWaveSteps x 64 entries
 #pragma unroll
-        for (int u = 0; u < kWaveSteps; ++u)
-            if (j0 + u < nsteps) step(j0 + u, dv[u], xv[u]);
-    }
+    for (int x = 0; x < kWaveSteps; ++x)
+        if ((uint32_t)x < nsteps) step(x, dv[x], xv[x]);
     bad = __ballot(bad) != 0 || nside > (uint32_t)kWaveSide;
     bool overflow = carry_k > sp.slot;
     // side fill: every side entry's products into its gap, in R's storage order
     if (!bad && (uint32_t)lane < nside) {
-        const uint64_t sw = R.W[s_sfj[lane]];
+        const uint64_t sw = R.SW[s_sfj[lane]];
         const uint32_t k0 = s_sfk[lane];
         if (k0 != 0xffffu) {
             const T x = s_sfx[lane];
@@ -2566,7 +1881,8 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     if (__ballot(overflow)) todo = 0;
     // exact path, one flagged row at a time, the whole wave on it: its products in sequence order
     // into the scratch, then every product checks for an earlier one of its column (first touch);
-    // a leader sums its group in order; kept leaders land in the row's slot range in that order
+    // a leader sums its group in order; kept leaders land in the row's slot range in that order.
+    // The row's descriptors come from the registers (entry e - E0 = step x, lane l: dv[x] of lane l)
     while (todo) {
         const int R0 = __builtin_ctzll(todo);
         todo &= todo - 1;
@@ -2575,14 +1891,18 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         for (uint32_t e0 = a0; e0 < a1; e0 += 64) {
             const uint32_t e = e0 + lane;
             const bool in = e < a1;
-            const uint32_t d = in ? DEt[e] : 0u;
+            // entries [e0, e0 + 64) lie in steps x0 = (e0 - E0) / 64 and x0 + 1
+            const uint32_t x0 = (e0 - E0) >> 6, src = (e - E0) & 63;
+            const uint32_t d0 = __shfl((int)reg_pick(dv, x0), (int)src, 64);
+            const uint32_t d1 = __shfl((int)reg_pick(dv, std::min(x0 + 1, (uint32_t)kWaveSteps - 1)), (int)src, 64);
+            const uint32_t d = in ? (((e - E0) >> 6) == x0 ? d0 : d1) : 0u;
             const T x = in ? Axt[e] : T(0);
             const uint32_t np = in ? ((d >> 30) < 3 ? (d >> 30) : (d >> 26) & 15u) : 0u;
             const uint32_t inc = wave_scan_dpp(np);
             const uint32_t q0 = nprod + inc - np;
             for (uint32_t t = 0; t < np; ++t)
                 if (q0 + t < (uint32_t)kWaveScr) {
-                    const uint32_t sl = lpr_slot_de(d, t, R.W, R.O);
+                    const uint32_t sl = lpr_slot_sw(d, t, R.SW, R.O);
                     scol[q0 + t] = (uint16_t)(sl & 0x3fffu);
                     sval[q0 + t] = tmul<T>(x, (sl & 0x4000u) ? -mag : mag);
                 }
@@ -2946,8 +2266,9 @@ struct rp_projector {
     int bs = 0;
     // packed
     DevBuf W, O, spare;  // packed image: W (u64 per feature), O (long-row records); spare unused
-    DevBuf W32;          // staged-gather table derived from W (u32 per feature), m < 2^30 only
-    DevBuf BM;           // nonempty-feature bitmap (1 bit per feature) for the filtered gather
+    DevBuf W32;          // staged-gather table derived from W (u32 per feature), m <= 2^26 only
+    DevBuf SW;           // side table: W words of the features with > 2 entries (W32 code 3)
+    DevBuf BM;           // nonempty-feature bitmap (1 bit per feature) for the staged gather
     int stage_mode = -1; // -1 auto, 0 off, 1 on (rp_projector_set_staging)
     int stage_sb = 0;    // bucket = 2^sb features; 0 = auto
     // rp_projector_set_option (tuning and tests; the library reads no environment variables)
@@ -2956,9 +2277,6 @@ struct rp_projector {
     int opt_defer_ticks = -1;   // -1 default
     int64_t opt_chunk_rows = 0; // 0 default
     int opt_host_threads = -1;  // -1 default
-    int opt_lpr_split = -1;     // -1 default (split), 0 the persistent main kernel, 1 split
-    int opt_filter = -1;        // -1 auto, 0 off, 1 on (filtered tile pipeline, RP_OPT_FILTER)
-    int64_t bm_nonempty = -1;   // features with at least one R entry (set bits of BM; -1: no BM)
     // generic
     DevBuf Bp, Bj, Bx32, Bx64;
     // internal workspace and host-path staging
@@ -3003,7 +2321,7 @@ size_t lds_bytes_for(const Caps& c, int value_size, int64_t p) {
 // Launch plan and workspace carve-up (offsets in bytes from the workspace start). Tile pipeline:
 //   [Workspace header + look-back states] [deferred list, pool offsets, headers, pool]. Row-lane:
 //   [header + scan states + heavy flags] [carry slots + gate] [wave counts, offsets, heavy list,
-//   row metadata, slots] [staged: OFFT, OFF2, GB, FILL, S, D, DE]   (value size vs: 8 when sizing)
+//   row metadata, slots] [staged: OFF2, CU, GB, FILL, S, D]   (value size vs: 8 when sizing)
 struct Plan {
     Caps caps;
     int64_t n_tiles = 0;
@@ -3011,7 +2329,7 @@ struct Plan {
     bool defer = false;
     int sb = 0, nb = 0;
     uint32_t ostride = 0;
-    size_t head = 0, dlist = 0, pofs = 0, dhdr = 0, pcols = 0, pvals = 0, offt = 0, s = 0, d = 0;
+    size_t head = 0, dlist = 0, pofs = 0, dhdr = 0, pcols = 0, pvals = 0, cu = 0, s = 0, d = 0;
     unsigned long long pool_cap = 0;
     size_t total = 0;
     // row-lane pipeline (lpr_*): tiles of kLprRows rows, every tile's output in a fixed slot
@@ -3027,14 +2345,7 @@ struct Plan {
     size_t off2 = 0, gb = 0, fill = 0;  // staged runs (lpr_reserve_kernel, lpr_partition_kernel)
     int64_t sd_words = 0;               // S / D capacity (words)
     unsigned groups = 0;
-    bool split = false;                 // staged: unsort (M1) + wave kernel (M2) instead of lpr_main_kernel
-    size_t de = 0;                      // M1 -> M2 descriptors, n_tiles x cap_a words
-    // filtered tile pipeline (filter_kernel, then the tile kernel on A'), per row chunk: A' of at
-    // most f_emax entries and f_rmax rows; filter units of f_rpu rows with their own look-back
-    bool filter = false;
-    int64_t f_emax = 0, f_rmax = 0, f_units = 0;
-    int f_rpu = 0;
-    size_t f_cnt = 0, f_probe = 0, f_ptr = 0, f_idx = 0, f_val = 0, f_mask = 0;  // f_cnt: unit counts, offsets, block sums
+    uint32_t ucap = 0;                  // staged: entries per 64-row unit on the fast path (<= 16 steps)
 };
 
 constexpr unsigned kDeferCopyGrid = 32768;  // copy workgroups (grid-stride over the deferred list)
@@ -3060,20 +2371,6 @@ int64_t lpr_chunk_rows(const rp_projector* h) {  // RP_OPT_CHUNK_ROWS: rounded u
         return std::max<int64_t>(kLprRows, (h->opt_chunk_rows + kLprRows - 1) / kLprRows * kLprRows);
     return kLprChunkRows;
 }
-// Filtered tile pipeline: packed R with a nonempty-feature bitmap (m <= 2^26), opt-in
-// (RP_OPT_FILTER = 1). Measured on configs[3]: 256.6 ms vs 235.1 unfiltered — the
-// bitmap lookups (2.0e10 random L2 hits at ~227 G/s: 88 ms) cost about what the 72% fewer W gathers
-// save (the tile kernel 226 -> 113 ms), and the compaction's write pass adds 48 ms; auto (-1) is off
-// until that changes
-constexpr int64_t kFiltMaxEntries = (int64_t)1 << 30;  // A' entries per row chunk (int32 row pointers)
-constexpr bool kFiltAuto = false;
-bool filter_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
-    if (h->layout != RP_LAYOUT_PACKED || !h->BM.p || h->bm_nonempty < 0 || n_rows <= 0 || nnz_a <= 0 ||
-        h->opt_filter == 0)
-        return false;
-    return h->opt_filter == 1 || (kFiltAuto && 2 * h->bm_nonempty <= h->m);
-}
-
 bool lpr_wanted(const rp_projector* h, int64_t n_rows, int64_t nnz_a) {
     if (h->layout != RP_LAYOUT_PACKED || n_rows <= 0 || nnz_a < 0) return false;
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
@@ -3121,7 +2418,14 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
         pl.total = pl.lvals + al((size_t)vs * (size_t)pl.lpr_slot * nw);
         const bool want_stage = h->stage_mode == 1 || (h->stage_mode == -1 && kLprStageAuto &&
                                                        nnz_a >= kStageMinNnz && 8 * h->m >= kStageMinTable);
-        if (allow_stage && want_stage && h->W32.p) {
+        // the wave kernel holds a unit's descriptors in registers, at most kWaveSteps x 64: a unit
+        // of 64 average rows plus 8 sigma must fit (KDD2012: 704 + 212 -> cap 1024, 12 sigma); a
+        // unit past the cap takes the exact heavy path with its tile. Rows of more than ~12.5
+        // entries on average take direct gathers instead.
+        const double ents_u = avg * 64, need_u = ents_u + 8.0 * std::sqrt(ents_u);
+        pl.ucap = (uint32_t)std::min<double>(64.0 * kWaveSteps, ((int)need_u + 63) & ~63);
+        const bool fits_u = need_u <= 64.0 * kWaveSteps;
+        if (allow_stage && want_stage && fits_u && h->W32.p) {
             int sb = h->stage_sb > 0 ? h->stage_sb : 19;
             auto nbk = [&](int b) { return (int)((h->m + ((int64_t)1 << b) - 1) >> b); };
             while (h->stage_sb <= 0 && nbk(sb) > kStageMaxNB && sb < 20) ++sb;
@@ -3135,9 +2439,9 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
                 // kernel's loads, instead of one line per bucket)
                 pl.ostride = (uint32_t)((pl.nb + 1 + 7) & ~7);
                 pl.groups = (unsigned)((pl.n_tiles + kRunGroup - 1) / kRunGroup);
-                pl.offt = pl.total;
-                pl.off2 = pl.offt + al(2 * (size_t)pl.ostride * (size_t)pl.n_tiles);
-                pl.gb = pl.off2 + al(4 * (size_t)pl.ostride * (size_t)pl.n_tiles);
+                pl.off2 = pl.total;
+                pl.cu = pl.off2 + al(4 * (size_t)pl.ostride * (size_t)pl.n_tiles);
+                pl.gb = pl.cu + al(2 * 4 * (size_t)pl.ostride * (size_t)pl.n_tiles);
                 const size_t nseg = (size_t)pl.groups * pl.nb;
                 pl.fill = pl.gb + al(8 * (nseg + 1));
                 // staged entries of one chunk: all of them, or (several chunks) at most cap_a per
@@ -3149,11 +2453,6 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
                 pl.s = pl.fill + al(4 * nseg);
                 pl.d = pl.s + al(4 * sd);
                 pl.total = pl.d + al(4 * sd);
-                pl.split = h->opt_lpr_split != 0;
-                if (pl.split) {
-                    pl.de = pl.total;
-                    pl.total = pl.de + al(4 * (size_t)pl.n_tiles * (size_t)pl.caps.cap_a);
-                }
             }
         }
         return pl;
@@ -3173,36 +2472,6 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
         pl.pcols = pl.dhdr + al(2 * (size_t)(pl.caps.rpt + 1) * (size_t)pl.n_tiles);
         pl.pvals = pl.pcols + al(2 * (size_t)pl.pool_cap);
         pl.total = pl.pvals + al((size_t)vs * (size_t)pl.pool_cap);
-    }
-    if (pl.n_tiles > 0 && allow_defer && allow_stage && filter_wanted(h, n_rows, nnz_a)) {
-        // filtered: everything per row chunk (A' of <= f_emax entries, <= f_rmax rows); the tile
-        // part sized for one row per tile (its caps are chosen per call from the kept fraction)
-        const size_t plain = pl.head;  // the unfiltered blocking fallback needs only the states
-        pl.filter = true;
-        const double avg = (double)nnz_a / (double)n_rows;
-        pl.f_emax = std::min<int64_t>(nnz_a + kFiltRound, kFiltMaxEntries);
-        pl.f_rmax = std::min<int64_t>(n_rows, (int64_t)(1.25 * (double)pl.f_emax / avg) + kBlock);
-        if (h->opt_chunk_rows > 0) pl.f_rmax = std::min<int64_t>(pl.f_rmax, h->opt_chunk_rows);  // tests
-        // units of ~4 rounds (16K entries for configs[3]): enough loads in flight per workgroup
-        pl.f_rpu = (int)std::max(1.0, std::min((double)kBlock, 4.0 * kFiltRound / (1.15 * avg)));
-        pl.f_rmax = std::min<int64_t>(pl.f_rmax, (int64_t)16384 * kFiltScanBlock * pl.f_rpu);  // one top scan
-        pl.f_units = (pl.f_rmax + pl.f_rpu - 1) / pl.f_rpu + 1;
-        const size_t rt = (size_t)pl.f_rmax;
-        pl.head = al(sizeof(Workspace) + 8 * rt);
-        pl.zero = pl.head;
-        pl.pool_cap = (unsigned long long)(1.02 * ppe * (double)pl.f_emax) + 65536ull;
-        pl.dlist = pl.head;
-        pl.pofs = pl.dlist + al(4 * rt);
-        pl.dhdr = pl.pofs + al(8 * rt);
-        pl.pcols = pl.dhdr + al(2 * 2 * rt + 2);
-        pl.pvals = pl.pcols + al(2 * (size_t)pl.pool_cap);
-        pl.f_cnt = pl.pvals + al((size_t)vs * (size_t)pl.pool_cap);
-        pl.f_probe = pl.f_cnt + al(8 * (size_t)pl.f_units + 8 * (size_t)(pl.f_units / kFiltScanBlock + 1));
-        pl.f_ptr = pl.f_probe + al(8 * (kFiltProbe + 2));
-        pl.f_idx = pl.f_ptr + al(4 * (rt + 1));
-        pl.f_val = pl.f_idx + al(4 * (size_t)pl.f_emax);
-        pl.f_mask = pl.f_val + al((size_t)vs * (size_t)pl.f_emax);
-        pl.total = std::max(pl.f_mask + al(8 * (size_t)(filter_mask_base(pl.f_emax, (unsigned)pl.f_units) + 2)), plain);
     }
     return pl;  // the tile pipeline gathers R's descriptors directly (its staged gather was removed)
 }
@@ -3233,11 +2502,11 @@ int defer_polls_setting(const rp_projector* h, const Caps& caps) {
 template <typename T, typename IP, typename OP, typename OI, typename RL, int WPE = 1>
 int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
                 int order, Workspace* ws, unsigned n_tiles, const Plan& pl, size_t lds,
-                hipStream_t st, const unsigned long long* cbase = nullptr) {
+                hipStream_t st) {
     if constexpr (WPE == 1 && std::is_same<T, float>::value && std::is_same<RL, PackedR>::value) {
         // 7 tiles per CU fit the LDS (static arrays ~1.6 KB per tile): take the 7-wave build
         if (lds + 2048 <= 160 * 1024 / 7)
-            return launch_main<T, IP, OP, OI, RL, 7>(R, mag, h, a, c, order, ws, n_tiles, pl, lds, st, cbase);
+            return launch_main<T, IP, OP, OI, RL, 7>(R, mag, h, a, c, order, ws, n_tiles, pl, lds, st);
     }
     HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, WPE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -3251,7 +2520,7 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
                        (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order,
                        ws, n_tiles, dfr, pl.defer ? defer_polls_setting(h, pl.caps) : -1,
-                       pl.defer ? defer_ticks_setting(h, pl.caps) : 0, cbase);
+                       pl.defer ? defer_ticks_setting(h, pl.caps) : 0);
     HIP_TRY(hipGetLastError());
     if (pl.defer) {
         hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, kDeferCopyGrid)), dim3(kBlock), 0,
@@ -3262,16 +2531,16 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
     return RP_OK;
 }
 
-size_t lpr_lds_bytes(int cap_a, size_t vs, uint32_t slot, bool staged) {
-    // staged: the slot buffers hold the run table (4 bytes per bucket + a 4096-bit map) in step A
-    const size_t bufs = std::max(((8 * (size_t)slot + 15) & ~size_t(15)) + 4 * vs * (size_t)slot,
-                                 staged ? (size_t)(4 * kStageMaxNB + 8 * 64) : (size_t)0);
-    return ((4 * (size_t)cap_a + 15) & ~size_t(15)) + bufs;
+size_t lpr_lds_bytes(int cap_a, size_t vs, uint32_t slot) {  // lpr_main_flat_kernel: descriptors + 4 slots
+    return ((4 * (size_t)cap_a + 15) & ~size_t(15)) + ((8 * (size_t)slot + 15) & ~size_t(15)) + 4 * vs * (size_t)slot;
 }
 
+// One row chunk of the row-lane pipeline. staged: reserve, partition, gather, wave kernel (which
+// takes direct gathers itself if a segment overflowed: the gate); direct: lpr_main_flat_kernel.
+// Then the heavy tiles' count, the scan of the wave counts, the copy and the heavy tiles' write.
 template <typename T, typename IP, typename OP, typename OI>
 int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
-                     Workspace* ws, const Plan& pl, hipStream_t st, int64_t chunk) {
+                     Workspace* ws, const Plan& pl, bool staged, hipStream_t st, int64_t chunk) {
     char* base = reinterpret_cast<char*>(ws);
     unsigned long long* carry = reinterpret_cast<unsigned long long*>(base + pl.carry);
     LprSpace sp{reinterpret_cast<uint32_t*>(base + pl.lcnt), reinterpret_cast<unsigned long long*>(base + pl.loff),
@@ -3283,15 +2552,12 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
     const IP* Ap = (const IP*)a->indptr;
     const T* Ax = (const T*)a->data;
     const unsigned t8 = (n_tiles + 7) / 8;
-    // staged: the gate word says whether this call's staged kernels run (lpr_choose_kernel in auto
-    // mode, 1 when staging is forced); a segment overflow in the partition clears it, and the direct
-    // kernel then takes the rest of the call
-    uint32_t* gate = pl.staged ? reinterpret_cast<uint32_t*>(base + pl.carry + 16) : nullptr;
-    LprStage stg{};
-    stg.gate = gate;
-    if (pl.staged) {
-        uint16_t* OFFT = reinterpret_cast<uint16_t*>(base + pl.offt);
+    if (staged) {
+        // the gate word: 1 unless a segment overflow in a partition (this chunk's or an earlier
+        // one's) cleared it; the wave kernel then gathers directly
+        uint32_t* gate = reinterpret_cast<uint32_t*>(base + pl.carry + 16);
         uint32_t* OFF2 = reinterpret_cast<uint32_t*>(base + pl.off2);
+        uint16_t* CU = reinterpret_cast<uint16_t*>(base + pl.cu);
         int64_t* GB = reinterpret_cast<int64_t*>(base + pl.gb);
         uint32_t* FILL = reinterpret_cast<uint32_t*>(base + pl.fill);
         uint32_t* Sw = reinterpret_cast<uint32_t*>(base + pl.s);
@@ -3299,12 +2565,12 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
         hipLaunchKernelGGL((lpr_reserve_kernel<IP>), dim3(1), dim3(kResBlock), 0, st, Ap, a->n_rows, (int)kLprRows,
                            (int64_t)h->m, pl.groups, pl.sb, pl.nb, pl.caps.cap_a, pl.sd_words, GB, FILL, gate);
         HIP_TRY(hipGetLastError());
-        const size_t plds = 4 * (size_t)kPartTiles * (size_t)pl.caps.cap_a;
+        const size_t plds = lpr_partition_lds_bytes(pl.caps.cap_a, pl.nb);
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_partition_kernel<IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)plds));
         const unsigned n_st = (n_tiles + kPartTiles - 1) / kPartTiles, s8 = (n_st + 7) / 8;
         hipLaunchKernelGGL((lpr_partition_kernel<IP>), dim3(8 * s8), dim3(kPBlock), plds, st, Ap, a->indices,
-                           a->n_rows, pl.caps, n_tiles, s8, pl.sb, pl.nb, pl.ostride, OFFT, OFF2,
+                           a->n_rows, pl.caps.cap_a, n_tiles, s8, pl.sb, pl.nb, pl.ostride, OFF2, CU,
                            (const int64_t*)GB, FILL, Sw, gate);
         HIP_TRY(hipGetLastError());
         const unsigned grid = 8u * (unsigned)((pl.nb + 7) / 8) * pl.groups;
@@ -3314,46 +2580,19 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
                            (const uint32_t*)h->BM.p, (const int64_t*)GB, (const uint32_t*)FILL, pl.sb, pl.nb,
                            pl.groups, (const uint32_t*)Sw, Dw, gate);
         HIP_TRY(hipGetLastError());
-        stg = LprStage{gate, nullptr, OFFT, OFF2, GB, Sw, Dw, pl.ostride, pl.nb};
-    }
-    const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot, pl.staged);
-    // persistent grid: as many workgroups as can be resident (a multiple of 8: each stays in its
-    // XCD's tile range), never more than the tiles
-    auto grid_for = [&](const void* fn) -> unsigned {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kLprRows, lds) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || cus < 8)
-            cus = 256;
-        const unsigned want = ((unsigned)(per_cu * cus) + 7u) & ~7u;
-        return std::min(want, 8u * t8);
-    };
-    if (pl.staged && pl.split) {
-        uint32_t* DE = reinterpret_cast<uint32_t*>(base + pl.de);
-        const size_t ulds = 4 * (size_t)kPartTiles * (size_t)pl.caps.cap_a;
-        HIP_TRY(hipFuncSetAttribute((const void*)lpr_unsort_kernel<IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)ulds));
-        const unsigned n_st = (n_tiles + kPartTiles - 1) / kPartTiles, s8 = (n_st + 7) / 8;
-        hipLaunchKernelGGL((lpr_unsort_kernel<IP>), dim3(8 * s8), dim3(kPBlock), ulds, st, Ap, a->n_rows, stg,
-                           pl.caps.cap_a, n_tiles, s8, DE);
-        HIP_TRY(hipGetLastError());
-        const size_t wlds = lpr_wave_lds_bytes(pl.lpr_slot, sizeof(T));
+        const LprStage stg{gate, (const uint32_t*)h->W32.p, OFF2, CU, GB, Sw, Dw, pl.ostride, pl.nb};
+        const size_t wlds = lpr_wave_lds_bytes(pl.lpr_slot, sizeof(T), pl.ucap, pl.nb);
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_wave_kernel<T, IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)wlds));
-        hipLaunchKernelGGL((lpr_wave_kernel<T, IP>), dim3(4 * n_tiles), dim3(64), wlds, st, R, mag, a->n_rows, Ap, Ax,
-                           (const uint32_t*)DE, (const uint32_t*)gate, pl.caps.cap_a, n_tiles, order, sp, ws);
-    } else if (pl.staged) {
-        const void* fn = (const void*)lpr_main_kernel<T, IP, true>;
+        hipLaunchKernelGGL((lpr_wave_kernel<T, IP>), dim3(8u * 4u * kPartTiles * s8), dim3(64), wlds, st, R, mag,
+                           a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, pl.ucap, n_tiles, s8, order, sp, ws);
+    } else {
+        const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot);
+        const void* fn = (const void*)lpr_main_flat_kernel<T, IP>;
         HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((lpr_main_kernel<T, IP, true>), dim3(grid_for(fn)), dim3(kLprRows), lds, st, R, mag,
-                           a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
-    }
-    {  // direct gathers (staged: runs iff the gate is 0 — the device chose them, or a segment overflowed)
-        stg.w32 = (const uint32_t*)h->W32.p;
-        const void* fn = (const void*)lpr_main_flat_kernel<T, IP, false>;
-        HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((lpr_main_flat_kernel<T, IP, false>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag,
-                           a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, n_tiles, t8, order, sp, ws);
+        hipLaunchKernelGGL((lpr_main_flat_kernel<T, IP>), dim3(8 * t8), dim3(kLprRows), lds, st, R, mag,
+                           a->n_rows, Ap, a->indices, Ax, (const uint32_t*)h->W32.p, pl.caps.cap_a, n_tiles, t8, order,
+                           sp, ws);
     }
     HIP_TRY(hipGetLastError());
     const size_t hl = heavy_lds_bytes(h->p, sizeof(T));
@@ -3383,19 +2622,33 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
 // The row-lane pipeline over chunks of pl.lpr_chunk rows (one chunk unless the launch is huge):
 // chunk k sees the rows [k * chunk, ...) as its own CSR (indptr offset, entries indexed through it),
 // writes its indptr slice and its entries at the running total of the chunks before it (a device
-// carry slot), and re-zeroes the per-chunk header and states first. All on one stream, no sync.
+// carry slot), and re-zeroes the per-chunk header and states first. All on one stream. In auto
+// staging mode lpr_choose_kernel samples the call's feature ids first and the host reads its
+// verdict (4 bytes: the call's one wait, which lets only the chosen branch's kernels launch); a
+// caller may pass the choice instead (*choice >= 0: 1 staged, 0 direct; the stream pipelines reuse
+// their first chunk's), and gets back what was chosen.
 template <typename T, typename IP, typename OP, typename OI>
 int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
-               Workspace* ws, const Plan& pl, hipStream_t st) {
+               Workspace* ws, const Plan& pl, hipStream_t st, int* choice) {
     const int64_t n = a->n_rows, step = std::max<int64_t>(pl.lpr_chunk, 1);
     uint32_t* gate = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + pl.carry + 16);
-    if (pl.gated && n > 0) {  // staged or direct for this call, decided on the device (K0)
-        hipLaunchKernelGGL((lpr_choose_kernel<IP>), dim3(1), dim3(1024), 0, st, (const IP*)a->indptr, a->indices, n,
-                           gate);
-        HIP_TRY(hipGetLastError());
-    } else if (pl.staged) {  // staging forced: on unless a segment overflows
-        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)gate, 1u, 1, st));
+    bool staged = pl.staged;
+    if (pl.gated && n > 0) {  // staged or direct for this call: sampled on the device, read here
+        if (choice && *choice >= 0) {
+            staged = *choice != 0;
+        } else {
+            hipLaunchKernelGGL((lpr_choose_kernel<IP>), dim3(1), dim3(1024), 0, st, (const IP*)a->indptr, a->indices, n,
+                               gate);
+            HIP_TRY(hipGetLastError());
+            uint32_t g = 0;
+            HIP_TRY(hipMemcpyAsync(&g, gate, 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(poll_stream(st));
+            staged = g != 0;
+        }
     }
+    if (choice) *choice = staged ? 1 : 0;
+    // the gate: staged until a segment overflows; 0 records a direct call (rp_project_choice)
+    if (pl.staged) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)gate, staged ? 1u : 0u, 1, st));
     int64_t k = 0;
     for (int64_t r0 = 0; r0 < n; r0 += step, ++k) {
         rp_csr_in sa = *a;
@@ -3405,97 +2658,7 @@ int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, con
         rp_csr_out sc = *c;
         sc.indptr = (OP*)c->indptr + r0;
         if (k > 0) HIP_TRY(hipMemsetAsync(ws, 0, pl.head, st));  // the carry slots follow the header
-        const int rc = launch_lpr_chunk<T, IP, OP, OI>(R, mag, h, &sa, &sc, order, ws, pl, st, k);
-        if (rc) return rc;
-    }
-    return RP_OK;
-}
-
-// The filtered tile pipeline. One probe (row pointers at kFiltProbe + 1 rows and
-// the kept fraction of kFiltSample entries; the call's one host sync) cuts the rows into chunks of
-// at most f_emax entries and f_rmax rows and sizes the tile kernel's caps for the kept entries.
-// Per chunk: filter_kernel A -> A' (workspace), then the tile kernel + deferred copy on A', its tile
-// 0 starting at ws->total (the entries of the chunks before; the header's error and total words
-// survive the per-chunk re-zeroing). A probe interval past f_emax entries (rows of > 2^30 / 4096
-// entries): the whole call runs unfiltered with the blocking look-back.
-template <typename T, typename IP, typename OP, typename OI>
-int launch_tile_filtered(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
-                         int order, Workspace* ws, unsigned n_tiles_plain, const Plan& pl, size_t lds_plain,
-                         hipStream_t st) {
-    char* base = reinterpret_cast<char*>(ws);
-    const IP* Ap = (const IP*)a->indptr;
-    const int64_t n = a->n_rows;
-    int64_t* probe = reinterpret_cast<int64_t*>(base + pl.f_probe);
-    hipLaunchKernelGGL((filter_probe_kernel<IP>), dim3(1), dim3(1024), 0, st, Ap, a->indices, n,
-                       (const uint32_t*)h->BM.p, probe);
-    HIP_TRY(hipGetLastError());
-    std::vector<int64_t> hp(kFiltProbe + 2);
-    HIP_TRY(hipMemcpyAsync(hp.data(), probe, 8 * hp.size(), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    auto row_of = [&](int64_t k) { return n * k / kFiltProbe; };
-    std::vector<int64_t> cut{0};
-    for (int64_t k0 = 0; k0 < kFiltProbe;) {
-        int64_t k = k0;
-        while (k < kFiltProbe && hp[k + 1] - hp[k0] <= pl.f_emax && row_of(k + 1) - row_of(k0) <= pl.f_rmax) ++k;
-        if (k == k0) {  // one probe interval holds more than f_emax entries: unfiltered, blocking
-            Plan pp = pl;
-            pp.filter = false;
-            pp.defer = false;
-            return launch_main<T, IP, OP, OI, PackedR>(R, mag, h, a, c, order, ws, n_tiles_plain, pp, lds_plain, st);
-        }
-        if (row_of(k) > cut.back()) cut.push_back(row_of(k));
-        k0 = k;
-    }
-    // tile caps for A': its average row and products per entry from the sampled kept fraction
-    const double kf = std::max((double)hp[kFiltProbe + 1], 1.0) / (double)kFiltSample;
-    const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
-    const int64_t nnz_all = hp[kFiltProbe] - hp[0];
-    Plan tp = pl;
-    tp.filter = false;
-    tp.defer = true;
-    tp.caps = choose_caps(n, std::max<int64_t>(1, (int64_t)(kf * (double)nnz_all)), ppe / kf);
-    const size_t lds = lds_bytes_for(tp.caps, sizeof(T), h->p);
-    if (lds > 160 * 1024 - 4096) return fail(RP_ERR_UNSUPPORTED, "p=%lld too large for the LDS accumulator", (long long)h->p);
-    uint32_t* ucnt = reinterpret_cast<uint32_t*>(base + pl.f_cnt);
-    uint32_t* uoff = ucnt + pl.f_units;
-    uint32_t* bsum = uoff + pl.f_units;
-    uint32_t* boff = bsum + (pl.f_units / kFiltScanBlock + 1);
-    int32_t* Fp = reinterpret_cast<int32_t*>(base + pl.f_ptr);
-    int32_t* Fj = reinterpret_cast<int32_t*>(base + pl.f_idx);
-    T* Fx = reinterpret_cast<T*>(base + pl.f_val);
-    uint64_t* kmask = reinterpret_cast<uint64_t*>(base + pl.f_mask);
-    HIP_TRY(hipMemsetAsync(base, 0, sizeof(Workspace), st));   // total (the running base) and error from 0
-    for (size_t q = 0; q + 1 < cut.size(); ++q) {
-        const int64_t r0 = cut[q], rows = cut[q + 1] - r0;
-        const unsigned units = (unsigned)((rows + pl.f_rpu - 1) / pl.f_rpu);
-        const unsigned tiles = (unsigned)((rows + tp.caps.rpt - 1) / tp.caps.rpt);
-        const unsigned nsb = (units + kFiltScanBlock - 1) / kFiltScanBlock;
-        if ((int64_t)units > pl.f_units || (int64_t)tiles > pl.f_rmax || nsb > 16384)
-            return fail(RP_ERR_UNSUPPORTED, "filter chunk past its plan");
-        // per chunk: the tile counter and states re-zeroed; error (+4) and total (+8) kept
-        HIP_TRY(hipMemsetAsync(base, 0, 4, st));
-        HIP_TRY(hipMemsetAsync(base + 16, 0, sizeof(Workspace) - 16 + 8 * (size_t)tiles, st));
-        const IP* Apc = Ap + r0;
-        const uint32_t* BM = (const uint32_t*)h->BM.p;
-        hipLaunchKernelGGL((filter_count_kernel<IP>), dim3(units), dim3(kBlock), 0, st, Apc, a->indices, rows,
-                           pl.f_rpu, BM, ucnt, kmask);
-        hipLaunchKernelGGL(filter_scan_kernel, dim3(nsb), dim3(kBlock), 0, st, (const uint32_t*)ucnt, units, uoff, bsum);
-        hipLaunchKernelGGL(filter_scan_top_kernel, dim3(1), dim3(1024), 0, st, (const uint32_t*)bsum, nsb, boff);
-        hipLaunchKernelGGL((filter_write_kernel<T, IP>), dim3(units), dim3(kBlock), 0, st, Apc, a->indices,
-                           (const T*)a->data, rows, pl.f_rpu, units, (const uint64_t*)kmask, (const uint32_t*)ucnt,
-                           (const uint32_t*)uoff, (const uint32_t*)boff, Fp, Fj, Fx);
-        HIP_TRY(hipGetLastError());
-        rp_csr_in fa = *a;
-        fa.n_rows = rows;
-        fa.indptr = Fp;
-        fa.indptr_type = RP_I32;
-        fa.indices = Fj;
-        fa.data = Fx;
-        fa.nnz = -1;
-        rp_csr_out sc = *c;
-        sc.indptr = (OP*)c->indptr + r0;
-        const int rc = launch_main<T, int32_t, OP, OI, PackedR>(R, mag, h, &fa, &sc, order, ws, tiles, tp, lds, st,
-                                                                &ws->total);
+        const int rc = launch_lpr_chunk<T, IP, OP, OI>(R, mag, h, &sa, &sc, order, ws, pl, staged, st, k);
         if (rc) return rc;
     }
     return RP_OK;
@@ -3504,10 +2667,9 @@ int launch_tile_filtered(const PackedR& R, T mag, rp_projector* h, const rp_csr_
 template <typename T, typename IP, typename OP, typename OI, typename RL>
 int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
                  int order, Workspace* ws, unsigned n_tiles, const Plan& pl, size_t lds,
-                 hipStream_t st) {
+                 hipStream_t st, int* choice) {
     if constexpr (std::is_same<RL, PackedR>::value) {
-        if (pl.lpr) return launch_lpr<T, IP, OP, OI>(R, mag, h, a, c, order, ws, pl, st);
-        if (pl.filter) return launch_tile_filtered<T, IP, OP, OI>(R, mag, h, a, c, order, ws, n_tiles, pl, lds, st);
+        if (pl.lpr) return launch_lpr<T, IP, OP, OI>(R, mag, h, a, c, order, ws, pl, st, choice);
     }
     return launch_main<T, IP, OP, OI, RL>(R, mag, h, a, c, order, ws, n_tiles, pl, lds, st);
 }
@@ -3515,10 +2677,10 @@ int launch_typed(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const 
 template <typename T, typename RL>
 int dispatch_idx(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c,
                  int order, Workspace* ws, unsigned n_tiles, const Plan& caps, size_t lds,
-                 hipStream_t st) {
+                 hipStream_t st, int* choice) {
     const bool ip64 = a->indptr_type == RP_I64, op64 = c->indptr_type == RP_I64,
                oi64 = c->indices_type == RP_I64;
-#define RP_L(IP, OP, OI) return launch_typed<T, IP, OP, OI, RL>(R, mag, h, a, c, order, ws, n_tiles, caps, lds, st)
+#define RP_L(IP, OP, OI) return launch_typed<T, IP, OP, OI, RL>(R, mag, h, a, c, order, ws, n_tiles, caps, lds, st, choice)
     if (!ip64 && !op64 && !oi64) RP_L(int32_t, int32_t, int32_t);
     if (!ip64 && op64 && !oi64) RP_L(int32_t, int64_t, int32_t);
     if (!ip64 && op64 && oi64) RP_L(int32_t, int64_t, int64_t);
@@ -3548,9 +2710,10 @@ int ensure_generic_values(rp_projector* h, int T) {
     return RP_OK;
 }
 
+// choice: the staging verdict of a row-lane call in auto mode (see launch_lpr); NULL or -1 = sample it
 int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
                         void* workspace, int64_t workspace_bytes, hipStream_t st,
-                        int64_t* total_nnz, int64_t nnz_a_hint) {
+                        int64_t* total_nnz, int64_t nnz_a_hint, int* choice = nullptr) {
     if (!a || !c) return fail(RP_ERR_INVALID, "NULL operand");
     if (a->n_rows < 0) return fail(RP_ERR_INVALID, "n_rows < 0");
     if (a->data_type != RP_F32 && a->data_type != RP_F64)
@@ -3577,7 +2740,8 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
             plan = make_plan(h, a->n_rows, nnz_a_hint, false, vs, false);
     }
     const Caps& caps = plan.caps;
-    const size_t lds = plan.lpr ? std::max(lpr_lds_bytes(caps.cap_a, (size_t)vs, plan.lpr_slot, plan.staged), heavy_lds_bytes(h->p, (size_t)vs))
+    const size_t lds = plan.lpr ? std::max({lpr_lds_bytes(caps.cap_a, (size_t)vs, plan.lpr_slot), heavy_lds_bytes(h->p, (size_t)vs),
+                                            plan.staged ? lpr_partition_lds_bytes(caps.cap_a, plan.nb) : (size_t)0})
                                 : lds_bytes_for(caps, dtype_size(a->data_type), h->p);
     if (lds > 160 * 1024 - 4096)
         return fail(RP_ERR_UNSUPPORTED, "p=%lld too large for the LDS accumulator (%zu bytes)",
@@ -3606,16 +2770,16 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
         return RP_OK;
     }
     if (h->layout == RP_LAYOUT_PACKED) {
-        PackedR R{(const uint64_t*)h->W.p, (const uint16_t*)h->O.p};
+        PackedR R{(const uint64_t*)h->W.p, (const uint16_t*)h->O.p, (const uint64_t*)h->SW.p};
         rc = a->data_type == RP_F64
-                 ? dispatch_idx<double, PackedR>(R, h->mag, h, a, c, order, ws, n_tiles, plan, lds, st)
-                 : dispatch_idx<float, PackedR>(R, (float)h->mag, h, a, c, order, ws, n_tiles, plan, lds, st);
+                 ? dispatch_idx<double, PackedR>(R, h->mag, h, a, c, order, ws, n_tiles, plan, lds, st, choice)
+                 : dispatch_idx<float, PackedR>(R, (float)h->mag, h, a, c, order, ws, n_tiles, plan, lds, st, choice);
     } else if (a->data_type == RP_F64) {
         GenericR<double> R{(const int32_t*)h->Bp.p, (const uint16_t*)h->Bj.p, (const double*)h->Bx64.p};
-        rc = dispatch_idx<double, GenericR<double>>(R, 0.0, h, a, c, order, ws, n_tiles, plan, lds, st);
+        rc = dispatch_idx<double, GenericR<double>>(R, 0.0, h, a, c, order, ws, n_tiles, plan, lds, st, choice);
     } else {
         GenericR<float> R{(const int32_t*)h->Bp.p, (const uint16_t*)h->Bj.p, (const float*)h->Bx32.p};
-        rc = dispatch_idx<float, GenericR<float>>(R, 0.0f, h, a, c, order, ws, n_tiles, plan, lds, st);
+        rc = dispatch_idx<float, GenericR<float>>(R, 0.0f, h, a, c, order, ws, n_tiles, plan, lds, st, choice);
     }
     if (rc) return rc;
     // what ran, for rp_project_choice: the row-lane gate when staged (the device's choice, or a
@@ -3745,12 +2909,6 @@ void image_parts(const HostImage& img, const void* data, int32_t data_type, cons
 // C-ABI
 extern "C" {
 
-#ifdef RP_STAMPS
-int rp_debug_stamps(void* dev_buf) {
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_buf, sizeof(void*)));
-    return RP_OK;
-}
-#endif
 
 const char* rp_last_error(void) { return g_err.c_str(); }
 const char* rp_version(void) { return "rp-mi355x 0.1 (gfx950)"; }
@@ -3782,8 +2940,19 @@ int build_w32(rp_projector* h) {
     if (h->layout != RP_LAYOUT_PACKED || h->m <= 0 || h->m > ((int64_t)1 << 26)) return RP_OK;
     int rc = h->W32.ensure(4 * (size_t)h->m, h->device);
     if (rc) return rc;
-    hipLaunchKernelGGL(build_w32_kernel, dim3(2048), dim3(256), 0, nullptr, (const uint64_t*)h->W.p,
-                       (const uint16_t*)h->O.p, (uint32_t*)h->W32.p, h->m);
+    // side table: count the features with > 2 entries per 1024-feature block, scan, then write
+    const int64_t nblk = (h->m + kSideBlock - 1) / kSideBlock;
+    DevBuf cnt, tmp;
+    if ((rc = cnt.ensure(8 * (size_t)nblk, h->device))) return rc;
+    hipLaunchKernelGGL(side_count_kernel, dim3((unsigned)nblk), dim3(kSideBlock), 0, nullptr,
+                       (const uint64_t*)h->W.p, h->m, (int64_t*)cnt.p);
+    HIP_TRY(hipGetLastError());
+    if ((rc = rpd::inclusive_scan_i64((int64_t*)cnt.p, nblk, nullptr, tmp, h->device))) return rc;
+    int64_t nside = 0;
+    HIP_TRY(hipMemcpy(&nside, (int64_t*)cnt.p + nblk - 1, 8, hipMemcpyDeviceToHost));
+    if ((rc = h->SW.ensure(8 * (size_t)std::max<int64_t>(nside, 1), h->device))) return rc;
+    hipLaunchKernelGGL(build_w32_kernel, dim3((unsigned)nblk), dim3(kSideBlock), 0, nullptr, (const uint64_t*)h->W.p,
+                       (const uint16_t*)h->O.p, (const int64_t*)cnt.p, (uint32_t*)h->W32.p, (uint64_t*)h->SW.p, h->m);
     HIP_TRY(hipGetLastError());
     // bitmap padded to whole 2^20-feature slices so a gather workgroup can stage any slice
     const size_t bm_words = (size_t)((h->m + (1 << 20) - 1) >> 20) << 15;
@@ -3793,15 +2962,7 @@ int build_w32(rp_projector* h) {
     hipLaunchKernelGGL(build_bitmap_kernel, dim3(2048), dim3(256), 0, nullptr, (const uint64_t*)h->W.p,
                        (uint32_t*)h->BM.p, h->m);
     HIP_TRY(hipGetLastError());
-    DevBuf cnt;  // nonempty features (the filtered tile pipeline's auto choice)
-    if ((rc = cnt.ensure(8, h->device))) return rc;
-    HIP_TRY(hipMemset(cnt.p, 0, 8));
-    hipLaunchKernelGGL(count_bits_kernel, dim3(256), dim3(256), 0, nullptr, (const uint32_t*)h->BM.p,
-                       (int64_t)bm_words, (unsigned long long*)cnt.p);
-    HIP_TRY(hipGetLastError());
-    unsigned long long nz = 0;
-    HIP_TRY(hipMemcpy(&nz, cnt.p, 8, hipMemcpyDeviceToHost));
-    h->bm_nonempty = (int64_t)nz;
+    HIP_TRY(hipDeviceSynchronize());  // cnt / tmp are released on return
     return RP_OK;
 }
 }  // namespace
@@ -3998,7 +3159,7 @@ int rp_project_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, int32_
                     int32_t* bucket_shift) {
     if (!h || n_rows < 0) return fail(RP_ERR_INVALID, "NULL projector or n_rows < 0");
     const Plan pl = make_plan(h, n_rows, nnz_a);
-    if (pipeline) *pipeline = pl.lpr ? RP_PIPE_ROWLANE : pl.filter ? RP_PIPE_TILE_FILTERED : RP_PIPE_TILE;
+    if (pipeline) *pipeline = pl.lpr ? RP_PIPE_ROWLANE : RP_PIPE_TILE;
     if (staged) *staged = pl.gated ? 2 : pl.staged ? 1 : 0;
     if (bucket_shift) *bucket_shift = pl.staged ? pl.sb : 0;
     return RP_OK;
@@ -4054,12 +3215,6 @@ int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value) {
         case RP_OPT_HOST_THREADS:
             h->opt_host_threads = (int)std::max<int64_t>(std::min<int64_t>(value, 256), -1);
             return RP_OK;
-        case RP_OPT_FILTER:
-            h->opt_filter = (int)std::max<int64_t>(std::min<int64_t>(value, 1), -1);
-            return RP_OK;
-        case RP_OPT_LPR_SPLIT:
-            h->opt_lpr_split = (int)std::max<int64_t>(std::min<int64_t>(value, 1), -1);
-            return RP_OK;
         default:
             return fail(RP_ERR_INVALID, "unknown option %d", option);
     }
@@ -4073,8 +3228,6 @@ int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* valu
         case RP_OPT_DEFER_TICKS: *value = h->opt_defer_ticks; return RP_OK;
         case RP_OPT_CHUNK_ROWS: *value = h->opt_chunk_rows; return RP_OK;
         case RP_OPT_HOST_THREADS: *value = h->opt_host_threads; return RP_OK;
-        case RP_OPT_LPR_SPLIT: *value = h->opt_lpr_split; return RP_OK;
-        case RP_OPT_FILTER: *value = h->opt_filter; return RP_OK;
         default: return fail(RP_ERR_INVALID, "unknown option %d", option);
     }
 }
@@ -4446,12 +3599,12 @@ int stream_upload(const rp_csr_in* a, const StreamChunk& ck, StreamSlot& s, hipS
 }
 
 int stream_project(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int order, int vt, int out_ip, int out_ix,
-                   unsigned long long* total, bool last, hipStream_t st);
+                   unsigned long long* total, bool last, hipStream_t st, int* choice);
 
 // the chunk's kernels on the compute stream; output capacity s.cap (the exact nnz lands in info[1])
 int stream_compute(rp_projector* h, const rp_csr_in* a, const StreamChunk& ck, StreamSlot& s, int order,
                    int ip_type, int vt,
-                   int out_ip, int out_ix, unsigned long long* total, bool last, hipStream_t st) {
+                   int out_ip, int out_ix, unsigned long long* total, bool last, hipStream_t st, int* choice) {
     unsigned long long* info = (unsigned long long*)s.info.p;
     const unsigned long long init[5] = {0, 0, ~0ull, ~0ull, 0};
     HIP_TRY(hipMemcpyAsync(info, init, sizeof init, hipMemcpyHostToDevice, st));
@@ -4478,17 +3631,18 @@ int stream_compute(rp_projector* h, const rp_csr_in* a, const StreamChunk& ck, S
     if (chk[2] != ~0ull)
         return fail(RP_ERR_INVALID, "A column index %d out of range [0, %lld)", a->indices[ck.e0 + (int64_t)chk[2]],
                     (long long)h->m);
-    return stream_project(h, ck, s, order, vt, out_ip, out_ix, total, last, st);
+    return stream_project(h, ck, s, order, vt, out_ip, out_ix, total, last, st, choice);
 }
 
 // the projection part of a chunk: its CSR is in s.ap (int64, from 0) / s.aj / s.ax on the device;
-// output offsets chained on the device through `total`
+// output offsets chained on the device through `total`; *choice: the staging verdict sampled on the
+// first chunk (-1 before it), reused by the others
 int stream_project(rp_projector* h, const StreamChunk& ck, StreamSlot& s, int order, int vt, int out_ip, int out_ix,
-                   unsigned long long* total, bool last, hipStream_t st) {
+                   unsigned long long* total, bool last, hipStream_t st, int* choice) {
     unsigned long long* info = (unsigned long long*)s.info.p;
     rp_csr_in ad{ck.rows, s.ap.p, RP_I64, (const int32_t*)s.aj.p, s.ax.p, vt, ck.nnz};
     rp_csr_out cd{s.cp.p, RP_I64, s.cj.p, RP_I32, s.cx.p, s.cap};
-    int rc = project_device_impl(h, &ad, &cd, order, s.ws.p, (int64_t)s.ws_need, st, nullptr, ck.nnz);
+    int rc = project_device_impl(h, &ad, &cd, order, s.ws.p, (int64_t)s.ws_need, st, nullptr, ck.nnz, choice);
     if (rc) return rc;
     hipLaunchKernelGGL(stream_finish_kernel, dim3(1), dim3(64), 0, st, (const Workspace*)s.ws.p, total, info);
     const int64_t np = ck.rows + (last ? 1 : 0);  // the next chunk writes the shared boundary entry
@@ -4571,6 +3725,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
     if (a->n_rows < 0 || !a->indptr || !c->indptr) return fail(RP_ERR_INVALID, "bad CSR arrays");
     if (c->capacity > 0 && (!c->indices || !c->data)) return fail(RP_ERR_INVALID, "NULL output arrays");
     const int64_t n = a->n_rows;
+    int choice = -1;  // staged or direct gathers: sampled on the first chunk, kept for the call
     if (chunk_rows <= 0) chunk_rows = kStreamChunkRows;
     // chunk plan from indptr at chunk boundaries (the rows inside a chunk are checked on the device)
     std::vector<StreamChunk> chunks;
@@ -4660,7 +3815,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
         if (!sy.wait([&] { return sy.uploaded > k && sy.downloaded >= k - ns + 1; })) break;
         if ((rc = stream_compute(h, a, chunks[(size_t)k], slots[k % ns], order, a->indptr_type, a->data_type,
                                  c->indptr_type, c->indices_type, (unsigned long long*)totbuf.p, k == K - 1,
-                                 st_comp))) {
+                                 st_comp, &choice))) {
             sy.set_error(rc);
             break;
         }
@@ -4691,7 +3846,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
             break;
         }
         if ((rc = stream_compute(h, a, ck, s, order, a->indptr_type, a->data_type, c->indptr_type, c->indices_type,
-                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp)))
+                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp, &choice)))
             break;
         int64_t kk = 0;
         bool rd = false;
@@ -4744,6 +3899,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
     if (!c->indptr || (c->capacity > 0 && (!c->indices || !c->data)) || (cap_rows > 0 && !labels))
         return fail(RP_ERR_INVALID, "NULL output arrays");
     if (chunk_bytes <= 0) chunk_bytes = 64ll << 20;
+    int choice = -1;  // staged or direct gathers: sampled on the first chunk, kept for the call
     std::vector<TextChunk> chunks;
     for (int64_t b = 0; b < n_bytes;) {
         int64_t e = std::min(n_bytes, b + chunk_bytes);
@@ -4873,7 +4029,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
             break;
         }
         if ((rc = stream_project(h, cks[(size_t)k], t.s, order, RP_F32, c->indptr_type, c->indices_type,
-                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp))) {
+                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp, &choice))) {
             sy.set_error(rc);
             break;
         }
@@ -4905,7 +4061,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
             break;
         }
         if ((rc = stream_project(h, cks[(size_t)k], t.s, order, RP_F32, c->indptr_type, c->indices_type,
-                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp)))
+                                 (unsigned long long*)totbuf.p, k == K - 1, st_comp, &choice)))
             break;
         int64_t kk = 0;
         bool rd = false;

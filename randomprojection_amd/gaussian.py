@@ -60,11 +60,13 @@ def prepare_operand(A, compute: str):
     return A
 
 
-def dense_project_device(X, C, out=None, compute: str = "fp32", stream=None, prepared_c: bool = False):
+def dense_project_device(X, C, out=None, compute: str = "fp32", stream=None, prepared_c: bool = False,
+                         variant: int = -1):
     """``X @ C.T`` for device tensors X (n x m) and C (p x m) on librp's MFMA GEMM
     (rp_dense_project_device): "fp32" (exact-f32 MFMA, f32 result), "bf16" (bf16 inputs, f32
     accumulate, f32 result) or "fp64" (f64 MFMA, f64 result). ``prepared_c``: C already went through
-    ``prepare_operand`` for this compute mode. Runs on ``stream`` (default: torch's current stream);
+    ``prepare_operand`` for this compute mode. ``variant``: -1 the default kernel, 0..11 another
+    measured tile variant for this call only. Runs on ``stream`` (default: torch's current stream);
     temporaries made here are tied to that stream, so the caching allocator never hands them out
     while the GEMM may still read them."""
     import ctypes
@@ -96,7 +98,7 @@ def dense_project_device(X, C, out=None, compute: str = "fp32", stream=None, pre
     code = {"bf16": nat.RP_BF16, "fp32": nat.RP_F32, "fp64": nat.RP_F64}[compute]
     nat.check(nat.load().rp_dense_project_device(
         X.device.index or 0, ctypes.c_void_p(Xc.data_ptr()), code, n, Xc.shape[1], ctypes.c_void_p(Cc.data_ptr()), p,
-        ctypes.c_void_p(y.data_ptr()), y.stride(0), ctypes.c_void_p(stream)))
+        ctypes.c_void_p(y.data_ptr()), y.stride(0), ctypes.c_void_p(stream), int(variant)))
     return y
 
 

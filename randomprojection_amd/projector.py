@@ -320,17 +320,17 @@ class Projector:
 
     def plan(self, n_rows: int, nnz_a: int = -1) -> dict:
         """The kernel pipeline ``project_device`` runs for this shape with a full workspace
-        (rp_project_plan): {"pipeline": "tile"|"tile_filtered"|"rowlane", "staged": bool | "auto"
-        (decided on the device per call, see ``choice``), "bucket_shift": int}."""
+        (rp_project_plan): {"pipeline": "tile"|"rowlane", "staged": bool | "auto" (decided per call
+        from a sample of the feature ids, see ``choice``), "bucket_shift": int}."""
         pipe, st, sb = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         nat.check(self._lib.rp_project_plan(self._h, int(n_rows), int(nnz_a), ctypes.byref(pipe), ctypes.byref(st),
                                             ctypes.byref(sb)))
-        return {"pipeline": {0: "tile", 1: "rowlane", 2: "tile_filtered"}[pipe.value],
+        return {"pipeline": {0: "tile", 1: "rowlane"}[pipe.value],
                 "staged": "auto" if st.value == 2 else bool(st.value), "bucket_shift": int(sb.value)}
 
     def choice(self, n_rows: int, nnz_a: int, workspace) -> bool:
         """After a completed ``project_device`` call with ``workspace`` (torch uint8 tensor): whether
-        it ran the staged gather (auto mode decides on the device per call)."""
+        it ran the staged gather (auto mode decides per call from a sample taken on the device)."""
         st = ctypes.c_int32()
         ptr = int(workspace.data_ptr()) if hasattr(workspace, "data_ptr") else int(workspace)
         nat.check(self._lib.rp_project_choice(self._h, int(n_rows), int(nnz_a), ctypes.c_void_p(ptr), ctypes.byref(st)))
@@ -343,18 +343,14 @@ class Projector:
 
     _OPTIONS = {"pipeline": nat.RP_OPT_PIPELINE, "defer_polls": nat.RP_OPT_DEFER_POLLS,
                 "defer_ticks": nat.RP_OPT_DEFER_TICKS, "chunk_rows": nat.RP_OPT_CHUNK_ROWS,
-                "host_threads": nat.RP_OPT_HOST_THREADS, "lpr_split": nat.RP_OPT_LPR_SPLIT,
-                "filter": nat.RP_OPT_FILTER}
-    _OPTION_DEFAULTS = {"pipeline": 0, "defer_polls": -2, "defer_ticks": -1, "chunk_rows": 0, "host_threads": -1,
-                        "lpr_split": -1, "filter": -1}
+                "host_threads": nat.RP_OPT_HOST_THREADS}
+    _OPTION_DEFAULTS = {"pipeline": 0, "defer_polls": -2, "defer_ticks": -1, "chunk_rows": 0, "host_threads": -1}
     _PIPELINES = {"auto": 0, "tile": 1, "rowlane": 2}
 
     def set_option(self, name: str, value):
         """Tuning / test option of this projector (rp_projector_set_option; results are identical
         under every setting): pipeline ("auto" | "tile" | "rowlane"), defer_polls, defer_ticks,
-        chunk_rows, host_threads, lpr_split (1 unsort + wave kernels, 0 the persistent main kernel),
-        filter (tile pipeline: -1 auto, 0 off, 1 drop A entries with empty R rows first);
-        ``None`` restores the default."""
+        chunk_rows, host_threads; ``None`` restores the default."""
         if name not in self._OPTIONS:
             raise ValueError(f"unknown option {name!r}; one of {sorted(self._OPTIONS)}")
         if value is None:

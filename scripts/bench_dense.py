@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--stream-chunks", type=int, default=24)
     ap.add_argument("--ring", type=int, default=3)
     ap.add_argument("--no-stream", action="store_true")
-    ap.add_argument("--variant", type=int, default=-1, help="librp dense tile variant (rp_dense_set_variant)")
+    ap.add_argument("--variant", type=int, default=-1, help="librp dense tile variant (rp_dense_project_device variant, per call)")
     ap.add_argument("--lib", default=None, help="another librp build (A/B measurements; its id is reported)")
     args = ap.parse_args()
 
@@ -49,7 +49,7 @@ def main():
 
     from randomprojection_amd import _native as nat
 
-    nat.check(nat.load(args.lib).rp_dense_set_variant(args.variant))
+    nat.load(args.lib)
     torch.cuda.set_device(0)
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[args.compute]
     C = torch.as_tensor(gaussian_random_matrix(args.p, args.m, random_state=123).astype("float32"), device="cuda")
@@ -66,7 +66,7 @@ def main():
             torch.mm(X, C.t(), out=out)
 
     def ours():
-        dense_project_device(X, C, out=out, compute=args.compute)
+        dense_project_device(X, C, out=out, compute=args.compute, variant=args.variant)
 
     res = {}
     for name, fn in (("librp_mfma", ours), ("torch_hipblaslt", torch_mm)):
@@ -85,7 +85,7 @@ def main():
     # spread over the block (two f32-accumulating GEMMs differ only in summation order)
     rows = torch.arange(0, args.chunk, max(1, args.chunk // 512), device="cuda")[:512]
     ref = X[rows].double() @ C.double().t()
-    dense_project_device(X, C, out=out, compute=args.compute)
+    dense_project_device(X, C, out=out, compute=args.compute, variant=args.variant)
     rel_ours = float((out[rows].double() - ref).norm() / ref.norm())
     torch_mm()
     rel_torch = float((out[rows].double() - ref).norm() / ref.norm())

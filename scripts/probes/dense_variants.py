@@ -1,4 +1,4 @@
-"""Probe: librp dense MFMA GEMM tile variants (rp_dense_set_variant) — correctness on a ragged shape
+"""Probe: librp dense MFMA GEMM tile variants (rp_dense_project_device variant, per call) — correctness on a ragged shape
 against an fp64 product, then TFLOP/s on the configs[4] block (131072 x 16384 -> 1024)."""
 import json
 import os
@@ -8,7 +8,6 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-from randomprojection_amd import _native as nat  # noqa: E402
 from randomprojection_amd.gaussian import dense_project_device  # noqa: E402
 
 variants = [int(v) for v in sys.argv[1].split(",")]
@@ -26,16 +25,15 @@ for comp in ("bf16", "fp32"):
     out = torch.empty(131072, 1024, device="cuda")
     ref = Xs.to(dt).double().cpu().numpy() @ Cs.to(dt).double().cpu().numpy().T
     for v in variants:
-        nat.check(nat.load().rp_dense_set_variant(v))
-        Y = dense_project_device(Xs, Cs, compute=comp).cpu().numpy()
+        Y = dense_project_device(Xs, Cs, compute=comp, variant=v).cpu().numpy()
         rel = float(np.linalg.norm(Y - ref) / np.linalg.norm(ref))
         for _ in range(2):
-            dense_project_device(X, C, out=out, compute=comp)
+            dense_project_device(X, C, out=out, compute=comp, variant=v)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(5):
-            dense_project_device(X, C, out=out, compute=comp)
+            dense_project_device(X, C, out=out, compute=comp, variant=v)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 5

@@ -1,8 +1,8 @@
 """Summarise a rocprofv3 session of bench.py (scripts/gpu_profile.sh) into profiles/.
 
 One projection step = the kernels of rp_project_device: the row-lane pipeline (lpr_* kernels, the
-default for short rows over a packed R; staged: reserve/partition/gather + unsort/wave) or the tile
-pipeline (spgemm_lookback_kernel + defer_copy_kernel, + filter_* when filtered). Reads
+default for short rows over a packed R; staged: reserve/partition/gather + wave) or the tile
+pipeline (spgemm_lookback_kernel + defer_copy_kernel). Reads
 gpurun_out/prof_<tag>_trace/*kernel_stats.csv and the separate PMC passes
 (gpurun_out/prof_<tag>_pmc_*/*counter_collection.csv) and writes
   profiles/<tag>_kernel_stats.csv      the rocprofv3 --stats summary (copied)
@@ -24,13 +24,12 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel", "filter_probe_kernel", "filter_count_kernel",
-                "filter_scan_top_kernel", "filter_scan_kernel", "filter_write_kernel",
-                "lpr_reserve_kernel", "lpr_partition_kernel", "lpr_gather_kernel", "lpr_unsort_kernel", "lpr_wave_kernel",
-                "lpr_main_kernel", "lpr_main_flat_kernel", "lpr_choose_kernel",
+STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel",
+                "lpr_reserve_kernel", "lpr_partition_kernel", "lpr_gather_kernel", "lpr_wave_kernel",
+                "lpr_main_flat_kernel", "lpr_choose_kernel",
                 "lpr_heavy_count_kernel", "lpr_scan_kernel",
                 "lpr_copy_kernel", "lpr_heavy_write_kernel")
-MAIN_KERNELS = ("lpr_wave_kernel", "lpr_main_kernel", "lpr_main_flat_kernel", "spgemm_lookback_kernel")
+MAIN_KERNELS = ("lpr_wave_kernel", "lpr_main_flat_kernel", "spgemm_lookback_kernel")
 
 
 def short(name):

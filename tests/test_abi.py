@@ -58,7 +58,7 @@ def test_touched_source_is_a_stale_library(tmp_path):
     from randomprojection_amd import build
 
     lib = nat.load()
-    for rel in build.DEPS:
+    for rel in build.HASHED:
         dst = tmp_path / rel
         dst.parent.mkdir(parents=True, exist_ok=True)
         shutil.copy(os.path.join(ROOT, rel), dst)
@@ -71,6 +71,19 @@ def test_touched_source_is_a_stale_library(tmp_path):
         assert "rebuild" in str(e)
     else:
         raise AssertionError("a touched source was not detected")
+
+
+def test_source_id_covers_flags():
+    """A compile flag (e.g. -ffp-contract, which the bit-exactness depends on) is part of the id."""
+    from randomprojection_amd import build
+
+    sid = build.source_id()
+    build.FLAGS.append("-DRP_TEST_FLAG")
+    try:
+        assert build.source_id() != sid
+    finally:
+        build.FLAGS.pop()
+    assert build.source_id() == sid
 
 
 def test_committed_traffic_matches_sources():

@@ -58,27 +58,24 @@ def test_mfma_kernel_ragged_shapes(compute, shape, variant):
     one) on ragged tiles (rows / columns past the block, m not a multiple of the K step: padded)
     against an fp64 product of the same (bf16-rounded) operands."""
     import torch
-    from randomprojection_amd import _native as nat
     from randomprojection_amd.gaussian import dense_project_device
 
     if compute == "fp64" and variant not in (-1, 10):
         pytest.skip("two f64 kernels: the ring (default) and the two-buffer one (variant 10)")
-    nat.check(nat.load().rp_dense_set_variant(variant))
 
     n, m, p = shape
     rng = np.random.default_rng(n + m + p)
     wdt = np.float64 if compute == "fp64" else np.float32
     X = torch.as_tensor(rng.standard_normal((n, m)).astype(wdt), device="cuda")
     C = torch.as_tensor(rng.normal(0, 1 / 32, (p, m)).astype(wdt), device="cuda")
-    Y = dense_project_device(X, C, compute=compute).cpu().numpy()
+    Y = dense_project_device(X, C, compute=compute, variant=variant).cpu().numpy()
     dt = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[compute]
     ref = X.to(dt).double().cpu().numpy() @ C.to(dt).double().cpu().numpy().T
     assert Y.shape == (n, p) and Y.dtype == wdt
     # north_star tolerances: fp32 1e-5 (K = 16384 f32 fma chains: ~2e-6 measured), fp64 1e-12
     assert _rel(Y, ref) < (1e-12 if compute == "fp64" else 1e-5)
     out = torch.full((n, p + 7), 7.0, device="cuda", dtype=torch.float64 if compute == "fp64" else torch.float32)[:, :p]
-    dense_project_device(X, C, out=out, compute=compute)
-    nat.check(nat.load().rp_dense_set_variant(-1))
+    dense_project_device(X, C, out=out, compute=compute, variant=variant)
     assert np.array_equal(out.cpu().numpy(), Y)
 
 

@@ -1,5 +1,6 @@
 """Staged gather: bucketed descriptor fetch for the row-lane pipeline (super-tile
-partition, filtered gather, unsort + wave kernels or the persistent main kernel), and the tile
+partition with per-unit run parts, bitmap-filtered gather, wave kernel reading its unit's parts of
+the runs), and the tile
 pipeline under the same staging requests (it gathers directly since round 4: a staging request is
 accepted and ignored there). Results must be bit-identical to the direct-gather kernels and to the
 oracle (CPU restatement of scipy csr_matmat) for every bucket width, order, dtype, tile shape and
@@ -275,18 +276,16 @@ def _rows(rng, k, pool, m, dtype=np.float32):
                           np.concatenate([[0], np.cumsum(k)])), shape=(n, m))
 
 
-def _check_rowlane_staged(R, A, shift, staged=True, split=None):
+def _check_rowlane_staged(R, A, shift, staged=True):
     """Row-lane pipeline with staging forced on: host path in both orders against the oracle, then
     the device path, whose workspace records whether the staged gather ran (`staged`) or a segment
-    past its reserve sent the call to the direct kernel. ``split``: 1 unsort + wave kernels (the
-    default), 0 the persistent main kernel."""
+    past its reserve sent the call to direct gathers."""
     import torch
 
     want = oracle_product(A, R)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     P = Projector(R)
     P.set_option("pipeline", "rowlane")
-    P.set_option("lpr_split", split)
     P.set_staging("on", shift)
     assert P.plan(A.shape[0], A.nnz) == {"pipeline": "rowlane", "staged": True, "bucket_shift": shift}
     assert_same_csr(P.matmul(A), *want)
@@ -322,14 +321,12 @@ def test_rowlane_staged_tile_of_3200_live_entries(R2m_p1k):
     _check_rowlane_staged(R, A, 16)
 
 
-@pytest.mark.parametrize("split", [0, 1])
-def test_rowlane_staged_split_edges(R2m_p1k, split):
-    """The split staged pipeline (lpr_unsort_kernel + lpr_wave_kernel) and the persistent main kernel
-    on the same edge cases: a 64-row unit of 2240 entries (past the wave kernel's 32 x 64 entries:
-    the tile goes to the exact heavy path) next to light units of its tile, a unit whose 64 rows each
+def test_rowlane_staged_wave_edges(R2m_p1k):
+    """The staged wave kernel on edge cases: a 64-row unit of 2240 entries (past the unit cap: the
+    tile goes to the exact heavy path) next to light units of its tile, a unit whose 64 rows each
     hold one feature with more than 2 R entries plus ordinary ones (more side entries than the
-    wave's side list: heavy), units of 13 steps (a second load round), empty rows, both orders."""
-    rng = np.random.default_rng(4 + split)
+    wave's side list: heavy), units of 13 steps, empty rows, both orders."""
+    rng = np.random.default_rng(5)
     R = R2m_p1k
     m = R.shape[0]
     rl = np.diff(R.indptr)
@@ -341,9 +338,26 @@ def test_rowlane_staged_split_edges(R2m_p1k, split):
     A = sp.vstack([kdd_like(rng, 5 * 256, m, values="normal"), big, _rows(rng, np.full(256, 13), np.arange(m), m),
                    sp.csr_matrix((70, m), dtype=np.float32), sidey.astype(np.float32),
                    kdd_like(rng, 7 * 256 + 9, m, values="normal")]).tocsr()
-    _check_rowlane_staged(R, A, 16, split=split)
-    _check_rowlane_staged(R, sp.vstack([kdd_like(rng, 9 * 256 + 5, m, mean=11.2, values="normal")]).tocsr(), 19,
-                          split=split)
+    _check_rowlane_staged(R, A, 16)
+    _check_rowlane_staged(R, sp.vstack([kdd_like(rng, 9 * 256 + 5, m, mean=11.2, values="normal")]).tocsr(), 19)
+
+
+@pytest.mark.parametrize("k", [15, 16, 17])
+def test_rowlane_staged_unit_cap(R2m_p1k, k):
+    """Units at the wave kernel's register cap: 64 rows of k entries (k = 16: exactly 16 steps of 64
+    = the cap, the fast path; 17: one step past it, the tile goes heavy; 15: one step below), with
+    side entries and repeated output columns, next to ordinary tiles; a run table with entries of
+    all four units in most buckets."""
+    rng = np.random.default_rng(1600 + k)
+    R = R2m_p1k
+    m = R.shape[0]
+    rl = np.diff(R.indptr)
+    side = np.flatnonzero(rl >= 3)
+    wide = (_rows(rng, np.full(64, k - 1), np.arange(m), m) + _rows(rng, np.ones(64, int), side, m)).tocsr()
+    wide.sort_indices()
+    A = sp.vstack([kdd_like(rng, 3 * 256 + 64, m, mean=11.2, values="normal"), wide.astype(np.float32),
+                   kdd_like(rng, 128 + 5 * 256, m, mean=11.2, values="normal")]).tocsr()
+    _check_rowlane_staged(R, A, 17)
 
 
 def test_rowlane_staged_dead_tiles_and_empty_rows(R2m_p1k):
