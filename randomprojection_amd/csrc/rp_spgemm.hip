@@ -1614,7 +1614,8 @@ __host__ __device__ inline size_t lpr_wave_region_a(uint32_t slot, size_t vs, ui
 }
 __host__ __device__ inline size_t lpr_wave_lds_bytes(uint32_t slot, size_t vs, uint32_t ucap, int nb) {
     const size_t scr = ((2 * (size_t)kWaveScr + 15) & ~size_t(15)) + vs * kWaveScr;
-    const size_t tab = 8 * (size_t)kWaveSteps + 4 * (size_t)std::max(nb, 1);
+    const size_t tab = (8 * (size_t)kWaveSteps + 4 * (size_t)std::max(nb, 1) + 15) & ~size_t(15);
+    // a multiple of 16 bytes: the next wave's regions (8-byte bitmap words, f64 values) stay aligned
     return lpr_wave_region_a(slot, vs, ucap) + std::max(scr, tab);
 }
 // t-th product's (sign << 14 | col) of an entry with descriptor d (code 3: side-table word)
@@ -1638,71 +1639,105 @@ __device__ __forceinline__ uint32_t reg_pick(const uint32_t (&v)[N], uint32_t x)
     }
     return r;
 }
-// f32: built for 8 waves per SIMD (64 VGPRs; SGPRs were the limit at 7); f64 unconstrained
-template <typename T, typename IP, int WPE = std::is_same<T, float>::value ? 8 : 1>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
+// f32: built for 7 waves per SIMD (72 VGPRs: the S/D words and the values in flight together; LDS
+// allows ~29 one-wave workgroups per CU anyway); f64 unconstrained.
+// WU waves per workgroup, each its own unit, no block barrier: WU = 4 kPartTiles puts a super-tile's
+// units on one CU at the same time, so the lines their parts of a run share are fetched once (one
+// wave per workgroup measured 31.4 GB of HBM reads per configs[1] pass: units of one super-tile ran
+// microseconds apart and ~9 MB of run lines per XCD were in flight against a 4 MB L2).
+constexpr int kWaveUnits = 4 * kPartTiles;
+#ifndef RP_WAVE_UNITS  // A/B builds (scripts/build_variant.py): 1 or kWaveUnits
+#define RP_WAVE_UNITS 1
+#endif
+#ifndef RP_WAVE_NT     // A/B builds: 1 = non-temporal S/D loads
+#define RP_WAVE_NT 0
+#endif
+template <typename T, typename IP, int WU, int WPE = std::is_same<T, float>::value ? 7 : 1>
+__global__ void __launch_bounds__(64 * WU) __attribute__((amdgpu_waves_per_eu(WPE)))
 lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
                 const T* __restrict__ Ax, LprStage stg, int cap_a, uint32_t ucap, unsigned n_tiles, unsigned s8,
                 int order, LprSpace sp, Workspace* ws) {
-    extern __shared__ __align__(16) unsigned char lds[];  // region A (descriptors, then slot), region B
-    __shared__ uint64_t s_flag[kWaveSteps];               // row-start bitmap over the unit's entries
-    __shared__ uint64_t s_susp;                           // rows flagged for the exact path
-    __shared__ uint16_t s_kst[64];
-    __shared__ uint8_t s_nz2row[64];
-    __shared__ uint16_t s_sfk[kWaveSide];                 // side entry's slot position (0xffff: zero x)
-    __shared__ T s_sfx[kWaveSide];                        // ... its value
-    __shared__ uint32_t s_sfj[kWaveSide];                 // ... its side-table index
+    extern __shared__ __align__(16) unsigned char lds_all[];  // per wave: region A (descriptors, then slot), B
+    __shared__ uint64_t s_flag_[WU][kWaveSteps];               // row-start bitmap over the unit's entries
+    __shared__ uint64_t s_susp_[WU];                           // rows flagged for the exact path
+    __shared__ uint16_t s_kst_[WU][64];
+    __shared__ uint8_t s_nz2row_[WU][64];
+    __shared__ uint16_t s_sfk_[WU][kWaveSide];                 // side entry's slot position (0xffff: zero x)
+    __shared__ T s_sfx_[WU][kWaveSide];                        // ... its value
+    __shared__ uint32_t s_sfj_[WU][kWaveSide];                 // ... its side-table index
+    const int wv = WU > 1 ? (int)(threadIdx.x >> 6) : 0, lane = threadIdx.x & 63;
+    uint64_t* s_flag = s_flag_[wv];
+    uint64_t& s_susp = s_susp_[wv];
+    uint16_t* s_kst = s_kst_[wv];
+    uint8_t* s_nz2row = s_nz2row_[wv];
+    uint16_t* s_sfk = s_sfk_[wv];
+    T* s_sfx = s_sfx_[wv];
+    uint32_t* s_sfj = s_sfj_[wv];
+    unsigned char* lds = lds_all + (size_t)wv * lpr_wave_lds_bytes(sp.slot, sizeof(T), ucap, stg.nb);
     // unit order follows the partition's XCD ranges: XCD x takes the units of super-tiles
     // [x * s8, (x + 1) * s8) in order (workgroup i runs on XCD i % 8)
-    const unsigned rb = (blockIdx.x & 7u) * (4u * kPartTiles * s8) + (blockIdx.x >> 3);
+    const unsigned rb = WU > 1 ? xcd_tile(blockIdx.x, s8) * WU + wv
+                               : (blockIdx.x & 7u) * (4u * kPartTiles * s8) + (blockIdx.x >> 3);
     if (rb >= 4 * n_tiles) return;
     const unsigned tile = rb >> 2, u = rb & 3;
-    const int lane = threadIdx.x;
     const int64_t row0 = (int64_t)rb * 64;
     if (row0 >= n_rows) {  // the last tile's empty units
         if (lane == 0) sp.cnt[rb] = 0u;
         return;
     }
-    const uint32_t staged = *stg.gate;  // uniform: 0 after a segment overflow (direct gathers)
     const int nrows = (int)std::min<int64_t>(64, n_rows - row0);
     const int64_t trow0 = (int64_t)tile * kLprRows;
     const int64_t ta = (int64_t)Ap[trow0];
     const int64_t tn = (int64_t)Ap[std::min<int64_t>(trow0 + kLprRows, n_rows)] - ta;
     const uint32_t E0 = (uint32_t)((int64_t)Ap[row0] - ta), E1 = (uint32_t)((int64_t)Ap[row0 + nrows] - ta);
-    const uint32_t rs = lane < nrows ? (uint32_t)((int64_t)Ap[row0 + lane] - ta) : E1;
+    const uint32_t rs0 = (uint32_t)((int64_t)Ap[row0 + std::min(lane, nrows)] - ta);  // straight-line load
+    const uint32_t rs = lane < nrows ? rs0 : E1;
     auto go_heavy = [&]() {  // the heavy path takes the whole tile (idempotent over its four units)
         if (lane == 0 && atomicOr(&sp.tflag[tile], 1u) == 0u) sp.hlist[atomicAdd(&ws->n_deferred, 1u)] = tile;
     };
+    // staged: this unit's part of tile run b is [c0, c1) of the run at GB[g, b] + OFF2[tile, b];
+    // the table loads need only the unit index, so they go out with the row pointers
+    const size_t gq = (size_t)(tile / kRunGroup) * stg.nb;
+    int64_t g0 = 0;
+    constexpr int kNBL = kStageMaxNB / 64;
+    uint32_t cnt[kNBL], src[kNBL];
+    // Loads below are straight-line (clamped addresses, results masked afterwards): a load guarded
+    // by its own branch made the compiler wait for it inside the branch (vmcnt(0) after every load).
+    // The run table is read whatever the gate says (its words are only used when staged)
+    {
+        g0 = stg.gb[gq];
+        const uint16_t* __restrict__ cu1 = stg.cu + ((size_t)tile * 4 + u) * stg.ostride;
+        const uint16_t* __restrict__ cu0 = u ? cu1 - stg.ostride : cu1;
+        const uint32_t* __restrict__ o2 = stg.off2 + (size_t)tile * stg.ostride;
+        const int64_t* __restrict__ gbq = stg.gb + gq;
+#pragma unroll
+        for (int h = 0; h < kNBL; ++h) {
+            const int b = std::min(64 * h + lane, stg.nb - 1);
+            const uint32_t c1 = cu1[b], c0 = u ? (uint32_t)cu0[b] : 0u;
+            const bool ok = 64 * h + lane < stg.nb;
+            cnt[h] = ok ? c1 - c0 : 0u;
+            src[h] = (uint32_t)(gbq[b] - g0) + o2[b] + c0;
+        }
+    }
+    const uint32_t staged = *stg.gate;  // uniform: 0 after a segment overflow (direct gathers)
     const uint32_t nu = E1 - E0, nsteps = (nu + 63) >> 6;
     if (tn > cap_a || nu > ucap) {  // uniform: the partition staged nothing / too many for the registers
         go_heavy();
         return;
     }
+    if (nu == 0) {  // uniform: 64 empty rows (or fewer at the end): nothing to gather or store
+        if (lane < nrows) sp.rowmeta[row0 + lane] = 0u;
+        if (lane == 0) sp.cnt[rb] = 0u;
+        return;
+    }
     const T* __restrict__ Axt = Ax + ta;
-    const uint32_t elast = nu > 0 ? E1 - 1 : E0;
+    const uint32_t elast = E1 - 1;
     uint32_t dv[kWaveSteps];
-    T xv[kWaveSteps];
+    T xv[kWaveSteps];  // lanes past the unit hold any value: their descriptors are 0 (no products)
     uint32_t* desc = reinterpret_cast<uint32_t*>(lds);
     const size_t ra = lpr_wave_region_a(sp.slot, sizeof(T), ucap);
+    constexpr int kW0 = 12;  // steps loaded unconditionally (KDD2012 units: 11-12); the rest if present
     if (staged) {
-        // this unit's part of tile run b: [c0, c1) of the run at GB[g, b] + OFF2[tile, b]
-        const size_t gq = (size_t)(tile / kRunGroup) * stg.nb;
-        const int64_t g0 = stg.gb[gq];
-        const uint16_t* __restrict__ cu = stg.cu + (size_t)tile * 4 * stg.ostride;
-        constexpr int kNBL = kStageMaxNB / 64;
-        uint32_t cnt[kNBL], src[kNBL];
-#pragma unroll
-        for (int h = 0; h < kNBL; ++h) {
-            const int b = 64 * h + lane;
-            cnt[h] = 0u;
-            src[h] = 0u;
-            if (b < stg.nb) {
-                const uint32_t c1 = cu[(size_t)u * stg.ostride + b];
-                const uint32_t c0 = u ? cu[(size_t)(u - 1) * stg.ostride + b] : 0u;
-                cnt[h] = c1 - c0;
-                src[h] = (uint32_t)(stg.gb[gq + b] - g0) + stg.off2[(size_t)tile * stg.ostride + b] + c0;
-            }
-        }
         // the unit's layout: runs in bucket order; run k (k-th nonempty bucket) starts at layout
         // position pos (bit pos of the start bitmap), its words at S/D index ksrc[k] + position
         uint64_t* sbm = reinterpret_cast<uint64_t*>(lds + ra);
@@ -1734,31 +1769,49 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         const uint32_t* __restrict__ St = stg.s + g0;
         const uint32_t* __restrict__ Dt = stg.d + g0;
         uint32_t sv[kWaveSteps];
-#pragma unroll
-        for (int x = 0; x < kWaveSteps; ++x) {
-            sv[x] = 0u;
-            dv[x] = 0u;
-            if ((uint32_t)x < nsteps) {  // uniform
-                const uint32_t p = std::min(64u * x + lane, nu - 1);
-                const uint32_t k = (uint32_t)__shfl((int)bpre, (int)(p >> 6), 64) +
-                                   (uint32_t)__popcll(sbm[p >> 6] & (~0ull >> (63 - (p & 63)))) - 1u;
-                const uint32_t i = ksrc[k] + p;
+        // plain loads: the neighbouring units of the super-tile read the same lines
+        auto sd_load = [&](int x) {
+            const uint32_t p = std::min(64u * x + lane, nu - 1);
+            const uint32_t k = (uint32_t)__shfl((int)bpre, (int)(p >> 6), 64) +
+                               (uint32_t)__popcll(sbm[p >> 6] & (~0ull >> (63 - (p & 63)))) - 1u;
+            const uint32_t i = ksrc[k] + p;
+            if (RP_WAVE_NT) {
                 sv[x] = __builtin_nontemporal_load(St + i);
                 dv[x] = __builtin_nontemporal_load(Dt + i);
+            } else {
+                sv[x] = St[i];
+                dv[x] = Dt[i];
             }
+        };
+#pragma unroll
+        for (int x = 0; x < kW0; ++x) sd_load(x);
+        if (nsteps > kW0) {  // uniform
+#pragma unroll
+            for (int x = kW0; x < kWaveSteps; ++x) sd_load(x);
         }
+        // each D word to its entry's place (lanes past the unit wrote the last word again: skipped)
 #pragma unroll
-        for (int x = 0; x < kWaveSteps; ++x)
-            if ((uint32_t)x < nsteps && 64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
+        for (int x = 0; x < kW0; ++x)
+            if (64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
+        if (nsteps > kW0) {  // uniform
 #pragma unroll
-        for (int x = 0; x < kWaveSteps; ++x) {  // the values: needed only by the flat pass
-            const uint32_t e = E0 + 64 * x + lane;
-            const T v = Axt[std::min(e, elast)];
-            xv[x] = e < E1 ? v : T(0);
+            for (int x = kW0; x < kWaveSteps; ++x)
+                if (64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
+        }
+        // the values (after the S/D words: issued earlier they and the S/D words did not fit the
+        // register budget together)
+#pragma unroll
+        for (int x = 0; x < kW0; ++x) xv[x] = Axt[std::min(E0 + 64 * x + lane, elast)];
+        if (nsteps > kW0) {  // uniform
+#pragma unroll
+            for (int x = kW0; x < kWaveSteps; ++x) xv[x] = Axt[std::min(E0 + 64 * x + lane, elast)];
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int x = 0; x < kWaveSteps; ++x) dv[x] = (uint32_t)x < nsteps && 64u * x + lane < nu ? desc[64 * x + lane] : 0u;
+        for (int x = 0; x < kWaveSteps; ++x) {
+            const uint32_t v = desc[std::min(64u * x + lane, nu - 1)];
+            dv[x] = 64u * x + lane < nu ? v : 0u;
+        }
         // every descriptor is in registers before the slot (region A) is written below
         __builtin_amdgcn_wave_barrier();
         __asm__ volatile("" ::: "memory");
@@ -1767,15 +1820,34 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         int32_t jv[kWaveSteps];
 #pragma unroll
         for (int x = 0; x < kWaveSteps; ++x) {
-            const uint32_t e = E0 + 64 * x + lane;
-            const int32_t j = Ajt[std::min(e, elast)];
-            const T v = Axt[std::min(e, elast)];
-            jv[x] = e < E1 ? j : -1;
-            xv[x] = e < E1 ? v : T(0);
+            const uint32_t e = std::min(E0 + 64 * x + lane, elast);
+            jv[x] = Ajt[e];
+            xv[x] = Axt[e];
         }
 #pragma unroll
-        for (int x = 0; x < kWaveSteps; ++x) dv[x] = jv[x] >= 0 ? stg.w32[jv[x]] : 0u;
+        for (int x = 0; x < kWaveSteps; ++x) {
+            const uint32_t w = stg.w32[jv[x]];
+            dv[x] = 64u * x + lane < nu ? w : 0u;
+        }
     }
+    // side entries (code 3) in entry order: their side-table words are requested now and used after
+    // the flat pass (which lists the same entries in the same order), so the gather's latency hides
+    // behind the pass
+    uint32_t nside_pre = 0;
+#pragma unroll
+    for (int x = 0; x < kWaveSteps; ++x) {
+        if ((uint32_t)x < nsteps) {  // uniform
+            const bool side = (dv[x] >> 30) == 3u && 64u * x + lane < nu;
+            const uint64_t sm = __ballot(side);
+            if (side) {
+                const uint32_t k = nside_pre + (uint32_t)__popcll(sm & ((1ull << lane) - 1ull));
+                if (k < (uint32_t)kWaveSide) s_sfj[k] = dv[x] & kW32J;
+            }
+            nside_pre += (uint32_t)__popcll(sm);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t side_w = (uint32_t)lane < std::min(nside_pre, (uint32_t)kWaveSide) ? R.SW[s_sfj[lane]] : 0ull;
     const uint32_t re = __shfl_down(rs, 1, 64);
     const uint32_t rend = lane == nrows - 1 ? E1 : (lane < nrows ? re : E1);
     const bool valid = lane < nrows;
@@ -1825,10 +1897,9 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         const uint64_t sm = __ballot(side);
         if (side) {
             const uint32_t k = nside + (uint32_t)__builtin_popcountll(sm & ((1ull << lane) - 1));
-            if (k < (uint32_t)kWaveSide) {
+            if (k < (uint32_t)kWaveSide) {  // (its side-table index: listed before the pass)
                 s_sfk[k] = kc ? (uint16_t)K : (uint16_t)0xffffu;
                 s_sfx[k] = x;
-                s_sfj[k] = d & kW32J;
             }
             if (np == 15) bad = true;  // 15 or more entries: the count is not exact -> heavy tile
         }
@@ -1844,7 +1915,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     bool overflow = carry_k > sp.slot;
     // side fill: every side entry's products into its gap, in R's storage order
     if (!bad && (uint32_t)lane < nside) {
-        const uint64_t sw = R.SW[s_sfj[lane]];
+        const uint64_t sw = side_w;
         const uint32_t k0 = s_sfk[lane];
         if (k0 != 0xffffu) {
             const T x = s_sfx[lane];
@@ -2581,11 +2652,13 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
                            pl.groups, (const uint32_t*)Sw, Dw, gate);
         HIP_TRY(hipGetLastError());
         const LprStage stg{gate, (const uint32_t*)h->W32.p, OFF2, CU, GB, Sw, Dw, pl.ostride, pl.nb};
-        const size_t wlds = lpr_wave_lds_bytes(pl.lpr_slot, sizeof(T), pl.ucap, pl.nb);
-        HIP_TRY(hipFuncSetAttribute((const void*)lpr_wave_kernel<T, IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)wlds));
-        hipLaunchKernelGGL((lpr_wave_kernel<T, IP>), dim3(8u * 4u * kPartTiles * s8), dim3(64), wlds, st, R, mag,
-                           a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, pl.ucap, n_tiles, s8, order, sp, ws);
+        constexpr int WU = RP_WAVE_UNITS;
+        const size_t wlds = WU * lpr_wave_lds_bytes(pl.lpr_slot, sizeof(T), pl.ucap, pl.nb);
+        HIP_TRY(hipFuncSetAttribute((const void*)lpr_wave_kernel<T, IP, WU>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)wlds));
+        hipLaunchKernelGGL((lpr_wave_kernel<T, IP, WU>), dim3(8u * (4u * kPartTiles / WU) * s8), dim3(64 * WU), wlds,
+                           st, R, mag, a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, pl.ucap, n_tiles, s8, order,
+                           sp, ws);
     } else {
         const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot);
         const void* fn = (const void*)lpr_main_flat_kernel<T, IP>;
