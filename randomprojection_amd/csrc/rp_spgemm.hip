@@ -850,15 +850,6 @@ lpr_reserve_kernel(const IP* __restrict__ Ap, int64_t n_rows, int rpt, int64_t m
     }
 }
 
-// largest b in [0, nb] with st[b] <= q (fixed trip count: 9 probes cover nb <= 256)
-__device__ __forceinline__ uint32_t run_of(const uint16_t* st, int nb, uint32_t q) {
-    uint32_t lo = 0;
-#pragma unroll
-    for (uint32_t step = 256; step; step >>= 1)
-        if (lo + step <= (uint32_t)nb && st[lo + step] <= q) lo += step;
-    return lo;
-}
-
 // K2: partition, one workgroup per SUPER-TILE of kPartTiles consecutive tiles (one 256-thread
 // part per tile). Each tile's entries are histogrammed by (unit, bucket) in LDS; the unit counts
 // give CU and each entry's place inside its tile's run of a bucket (its unit's part: a cursor per
@@ -875,13 +866,14 @@ constexpr int kPBlock = kBlock * kPartTiles;
 static_assert(kRunGroup % kPartTiles == 0, "a super-tile never straddles two groups");
 // dynamic LDS: [the ranked S words [kPartTiles][cap_a], aliased by the unit histograms
 // [kPartTiles][4][nb] (dead by then)] [cursors [kPartTiles][4][nb]] [run destinations
-// [kPartTiles][nb] (i64)] [bucket starts [kPartTiles][nb + 1] (u16)]
+// [kPartTiles][nb] (i64)] [bucket starts [kPartTiles][nb + 1] (u16)] [each ranked word's bucket
+// [kPartTiles][cap_a] (u8): the store loop finds its run without a search]
 __host__ __device__ inline size_t lpr_partition_keys_bytes(int cap_a, int nb) {
     return (std::max<size_t>(4 * (size_t)kPartTiles * (size_t)cap_a, 16 * (size_t)kPartTiles * (size_t)nb) + 15) & ~size_t(15);
 }
 __host__ __device__ inline size_t lpr_partition_lds_bytes(int cap_a, int nb) {
     return lpr_partition_keys_bytes(cap_a, nb) + 16 * (size_t)kPartTiles * nb + 8 * (size_t)kPartTiles * nb +
-           ((2 * (size_t)kPartTiles * (nb + 1) + 15) & ~size_t(15));
+           ((2 * (size_t)kPartTiles * (nb + 1) + 15) & ~size_t(15)) + (((size_t)kPartTiles * cap_a + 15) & ~size_t(15));
 }
 template <typename IP>
 __global__ void __launch_bounds__(kPBlock)
@@ -908,6 +900,8 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
     uint32_t* s_cur = reinterpret_cast<uint32_t*>(dyn);  // per (tile, unit, bucket): next slot in the layout
     int64_t* s_dst = reinterpret_cast<int64_t*>(dyn + 16 * (size_t)kPartTiles * nb);  // per (tile, bucket)
     uint16_t* s_st = reinterpret_cast<uint16_t*>(dyn + 24 * (size_t)kPartTiles * nb);  // per tile: nb + 1
+    uint8_t* s_bk = reinterpret_cast<uint8_t*>(dyn + 24 * (size_t)kPartTiles * nb +
+                                               ((2 * (size_t)kPartTiles * (nb + 1) + 15) & ~size_t(15)));
     int64_t ea = 0, ne = 0;
     uint32_t u1 = 0, u2 = 0, u3 = 0;  // first entries of units 1..3 (tile-relative)
     if (live) {
@@ -996,6 +990,7 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
             const uint32_t f = (uint32_t)jj[i] & kW32J;
             const uint32_t pos = atomicAdd(&cur[((uint32_t)jj[i] >> 27) * nb + (f >> sb)], 1u);
             sk[pos] = (e << 20) | (f & mask);
+            s_bk[(size_t)q * cap_a + pos] = (uint8_t)(f >> sb);
         }
     if (q == 0 && qt < nb) {  // the super-tile's runs of bucket qt, adjacent in tile order
         uint32_t run = claim;
@@ -1014,8 +1009,8 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
         if (tid == 0) *gate = 0;
         return;
     }
-    const uint16_t* stq = s_st + q * (nb + 1);
-    for (uint32_t pos = qt; pos < n; pos += kBlock) S[s_dst[q * nb + run_of(stq, nb, pos)] + pos] = sk[pos];
+    const uint8_t* bkq = s_bk + (size_t)q * cap_a;
+    for (uint32_t pos = qt; pos < n; pos += kBlock) S[s_dst[q * nb + bkq[pos]] + pos] = sk[pos];
 }
 
 // K3: gather, one workgroup per (bucket b, group g) segment, on XCD b % 8 (workgroup i
@@ -1142,7 +1137,7 @@ struct LprSpace {
     unsigned long long* off;  // 4 x n_tiles: exclusive prefix of cnt (+ base)
     uint32_t* hlist;      // heavy tiles, count in ws->n_deferred
     uint32_t* tflag;      // n_tiles: 1 = heavy (lpr_heavy_write places the tile)
-    uint32_t* rowmeta;    // n_tiles x 256: the row's offset in its wave's output run (lpr_store_rows)
+    uint32_t* rowmeta;    // n_tiles x 256: the row's slot range, kst | kept << 16 (lpr_store_slot)
     uint16_t* cols;       // 4 x n_tiles x slot
     unsigned char* vals;  // 4 x n_tiles x slot x sizeof(T)
     unsigned long long* scan_state;  // one per 4096-wave scan block
@@ -1176,38 +1171,23 @@ __device__ __forceinline__ bool lpr_bloom(const uint16_t* cb, uint32_t kst, uint
     return hit;
 }
 
-// A wave's rows to HBM in their final order, back to back (row r's kept entries [kst, kst + kept)
-// of the LDS slot, reversed for scipy's reverse first-touch order or as built for RP_ORDER_SORTED;
-// gaps the exact path left between rows are squeezed out), so that the copy kernel moves one
-// contiguous run per wave. rowpre[lane] = the row's offset in the run, *cnt = the run's length.
+// A wave's slot to HBM as built (row r's kept entries at [kst, kst + kept), in first-touch order,
+// or ascending for RP_ORDER_SORTED; entries the exact path dropped leave gaps): `extent` entries
+// copied coalesced, each row's (kst, kept) in rowmeta, the run's entry count in *cnt. The copy
+// kernel puts each row in its final place and order (reversed for scipy's reverse first-touch
+// order): that per-output row search runs there, in a memory-bound kernel, not here.
 template <typename T>
-__device__ __forceinline__ void lpr_store_rows(const uint16_t* cb, const T* vb, uint32_t kst, uint32_t kept,
-                                               bool valid, int lane, int order, uint32_t* __restrict__ rowpre,
-                                               uint32_t* __restrict__ cnt, uint16_t* __restrict__ oc,
-                                               T* __restrict__ ov) {
+__device__ __forceinline__ void lpr_store_slot(const uint16_t* cb, const T* vb, uint32_t kst, uint32_t kept,
+                                               bool valid, int lane, uint32_t extent,
+                                               uint32_t* __restrict__ rowmeta, uint32_t* __restrict__ cnt,
+                                               uint16_t* __restrict__ oc, T* __restrict__ ov) {
     const uint32_t c = valid ? kept : 0u;
-    const uint32_t inc = wave_scan_dpp(c);
-    const uint32_t pre = inc - c;
-    const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
-    if (valid) rowpre[lane] = pre;
+    const uint32_t tot = __builtin_amdgcn_readlane(wave_scan_dpp(c), 63);
+    if (valid) rowmeta[lane] = kst | (c << 16);
     if (lane == 0) *cnt = tot;
-    for (uint32_t o0 = 0; o0 < tot; o0 += 64) {  // wave-uniform trip count: every lane shuffles
-        const uint32_t o = o0 + lane;
-        // the row holding output o: the last lane whose prefix is <= o (empty rows before it share
-        // its prefix; rows after it start past o)
-        int lo = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const uint32_t pv = __shfl(pre, lo + step, 64);
-            if (lo + step < 64 && pv <= o) lo += step;
-        }
-        const uint32_t rp = __shfl(pre, lo, 64), rk = __shfl(kst, lo, 64), rc = __shfl(c, lo, 64);
-        if (o < tot) {
-            const uint32_t i = o - rp;
-            const uint32_t src = order == RP_ORDER_SORTED ? rk + i : rk + rc - 1 - i;
-            __builtin_nontemporal_store(cb[src], oc + o);
-            __builtin_nontemporal_store(vb[src], ov + o);
-        }
+    for (uint32_t o = lane; o < extent; o += 64) {
+        __builtin_nontemporal_store(cb[o], oc + o);
+        __builtin_nontemporal_store(vb[o], ov + o);
     }
 }
 
@@ -1579,7 +1559,7 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     }
     __builtin_amdgcn_wave_barrier();
     const size_t wt = (size_t)tile * 4 + w;
-    lpr_store_rows<T>(cb, vb, kst, kept, valid, lane, order, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
+    lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
                       sp.cnt + wt, sp.cols + wt * sp.slot, reinterpret_cast<T*>(sp.vals) + wt * sp.slot);
 }
 
@@ -2034,7 +2014,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         }
     }
     __builtin_amdgcn_wave_barrier();
-    lpr_store_rows<T>(cb, vb, kst, kept, valid, lane, order, sp.rowmeta + row0, sp.cnt + rb,
+    lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, sp.rowmeta + row0, sp.cnt + rb,
                       sp.cols + (size_t)rb * sp.slot, reinterpret_cast<T*>(sp.vals) + (size_t)rb * sp.slot);
 }
 
@@ -2125,13 +2105,16 @@ lpr_scan_kernel(LprSpace sp, size_t n, const unsigned long long* __restrict__ ba
     }
 }
 
-// runs -> C: one workgroup per tile (grid-stride), one wave per 64-row unit: the unit's run (rows
-// already in their final order, back to back: lpr_store_rows) copied to its offset, indptr from
-// the rows' offsets in the run. Heavy tiles are placed by lpr_heavy_write_kernel.
+// slots -> C: one workgroup per tile (grid-stride), one wave per 64-row unit. The unit's rows (slot
+// ranges kst | kept << 16 in rowmeta) get their output offsets from a wave scan of the kept counts
+// (indptr); each output o finds its row (the last lane whose offset is <= o: empty rows share the
+// next row's offset) and reads its entry from the slot, the row reversed for scipy's reverse
+// first-touch order or as built (ascending) for RP_ORDER_SORTED. kCopyU steps of 64 outputs are
+// loaded before any is stored. Heavy tiles are placed by lpr_heavy_write_kernel.
 template <typename T, typename OP, typename OI>
 __global__ void __launch_bounds__(kBlock)
 lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ Cp, OI* __restrict__ Cj,
-                T* __restrict__ Cx, unsigned long long capacity) {
+                T* __restrict__ Cx, unsigned long long capacity, int order) {
     const T* vals = reinterpret_cast<const T*>(sp.vals);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (unsigned tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -2142,28 +2125,42 @@ lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ 
         const int64_t row0 = (int64_t)tile * kLprRows;
         const int nrows = (int)std::min<int64_t>(kLprRows, n_rows - row0);
         const int r = 64 * w + lane;
-        if (r < nrows) Cp[row0 + r] = (OP)(G + sp.rowmeta[row0 + r]);
+        const uint32_t meta = r < nrows ? sp.rowmeta[row0 + r] : 0u;
+        const uint32_t kst = meta & 0xffffu, kept = meta >> 16;
+        const uint32_t pre = wave_scan_dpp(kept) - kept;
+        if (r < nrows) Cp[row0 + r] = (OP)(G + pre);
         if (tile == n_tiles - 1 && threadIdx.x == kBlock - 1) Cp[n_rows] = (OP)(G + cnt);
         if (G + cnt > capacity) continue;
         const uint16_t* __restrict__ sc = sp.cols + wt * sp.slot;
         const T* __restrict__ sv = vals + wt * sp.slot;
-        // kCopyU steps of 64 entries loaded before any is stored (a run is ~6 steps: one round trip)
+        // the row's first slot entry and the step to the next output: reversed (scipy) or forward
+        const bool rev = order != RP_ORDER_SORTED;
+        const uint32_t base = rev ? kst + kept - 1 : kst;
         constexpr int kCopyU = 8;
-        for (uint32_t q0 = 0; q0 < cnt; q0 += 64 * kCopyU) {
+        for (uint32_t q0 = 0; q0 < cnt; q0 += 64 * kCopyU) {  // wave-uniform trip count
             uint16_t cv[kCopyU];
             T xv[kCopyU];
 #pragma unroll
             for (int u = 0; u < kCopyU; ++u) {
-                const uint32_t q = q0 + 64 * u + lane;
-                cv[u] = q < cnt ? __builtin_nontemporal_load(sc + q) : (uint16_t)0;
-                xv[u] = q < cnt ? __builtin_nontemporal_load(sv + q) : T(0);
+                const uint32_t o = q0 + 64 * u + lane;
+                int lo = 0;
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1) {
+                    const uint32_t pv = (uint32_t)__shfl((int)pre, lo + step, 64);
+                    if (lo + step < 64 && pv <= o) lo += step;
+                }
+                const uint32_t i = o - (uint32_t)__shfl((int)pre, lo, 64);
+                const uint32_t b = (uint32_t)__shfl((int)base, lo, 64);
+                const uint32_t src = std::min(rev ? b - i : b + i, sp.slot - 1);
+                cv[u] = o < cnt ? __builtin_nontemporal_load(sc + src) : (uint16_t)0;
+                xv[u] = o < cnt ? __builtin_nontemporal_load(sv + src) : T(0);
             }
 #pragma unroll
             for (int u = 0; u < kCopyU; ++u) {
-                const uint32_t q = q0 + 64 * u + lane;
-                if (q < cnt) {
-                    Cj[G + q] = (OI)cv[u];
-                    Cx[G + q] = xv[u];
+                const uint32_t o = q0 + 64 * u + lane;
+                if (o < cnt) {
+                    Cj[G + o] = (OI)cv[u];
+                    Cx[G + o] = xv[u];
                 }
             }
         }
@@ -2681,7 +2678,7 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL((lpr_copy_kernel<T, OP, OI>), dim3(std::min<unsigned>(n_tiles, 1u << 20)), dim3(kBlock), 0, st,
                        sp, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices, (T*)c->data,
-                       (unsigned long long)c->capacity);
+                       (unsigned long long)c->capacity, order);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipFuncSetAttribute((const void*)lpr_heavy_write_kernel<T, IP, OP, OI>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl));
