@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 per direction (measured copies: H2D ~55 GB/s, scripts/probes/pcie_probe2.hip)
 RANDOM_LINE_CEILING = 55e9  # random 128-B line fills/s, measured (scripts/probes/gather_probe*.hip)
 
 
@@ -159,6 +160,9 @@ def main():
     ap.add_argument("--host-mem", choices=["pageable", "pinned"], default="pinned",
                     help="--boundary host: host arrays in pageable (numpy) or page-locked (rp_host_alloc) memory")
     ap.add_argument("--chunk-rows", type=int, default=0, help="--boundary host: rows per chunk (0 = library default)")
+    ap.add_argument("--host-steps", type=int, default=None,
+                    help="device line: timed passes of the boundary-2 leg (host CSR stream) on the same rows "
+                         "after the device-resident measurement (default 3 for --config kdd, else 0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
@@ -173,6 +177,8 @@ def main():
         args.rows = 20_000_000  # ~5 GB of text in host memory per rank
     if args.boundary == "partition" and args.rows is None:
         args.rows = args.part_rows
+    if args.host_steps is None:
+        args.host_steps = 3 if args.config == "kdd" else 0
     for k in ("rows", "m", "p", "dist", "cpu_sample_rows"):
         if getattr(args, k) is None:
             setattr(args, k, cfg[k])
@@ -346,6 +352,18 @@ def main():
     if rank == 0 and not args.no_cpu_baseline:  # host cores, rank 0 only, the other ranks wait
         cpu = cpu_baseline(args, Ap, Aj, Ax, R_all)
     _barrier(dev)
+    # boundary 2 beside the headline: the same rows streamed host CSR -> host CSR (PCIe-inclusive);
+    # `value` stays the device-resident rate
+    boundaries = None
+    if args.host_steps > 0:
+        h = host_stream_leg(args, P, R_all, Ap, Aj, Ax, world, rank, dev, args.host_steps, 1)
+        boundaries = {"host": {
+            "rows_per_s": args.rows * world / h["dt"], "ms_per_pass": h["dt"] * 1e3, "steps": args.host_steps,
+            "link_frac": h["h2d"] / h["dt"] / 1e9 / PCIE_PEAK_GBS, "h2d_GBps_per_gpu": h["h2d"] / h["dt"] / 1e9,
+            "d2h_GBps_per_gpu": h["d2h"] / h["dt"] / 1e9, "host_mem": args.host_mem,
+            "entry": "rp_project_stream (include/rp.h), host CSR in -> host CSR out, PCIe-inclusive",
+            "verified": {"sample_rows_per_rank": h["sample_rows"], "sample_bitexact_vs_oracle": bool(h["same"]),
+                         "indptr_ok": bool(h["ptr_ok"]), "nnz_out_equal_device_leg": h["nnz_c"] == nnz_c}}}
 
     # rocprofv3 PMC results of a profiling session of this same workload on THIS build (profiles/):
     # HBM bytes per step and the L2 hit rate of the main kernel. A traffic file applies only when
@@ -405,6 +423,7 @@ def main():
                              (req * 1e9 / RANDOM_LINE_CEILING) if req else None},
             "cpu_baseline": cpu,
             "verified": check,
+            "boundaries": boundaries,
             "librp": {"build_id": LIB_ID, "checked_against_sources": LIB_CHECKED, "path": nat.loaded_path()},
             **args.dist_info,
             "r_setup_s": t_r,
@@ -497,13 +516,13 @@ def _r_host(args, R_host):
     return sp.csr_matrix((ix, ij, ip), shape=(m, p))
 
 
-def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
+def host_stream_leg(args, P, R_host, Ap, Aj, Ax, world, rank, dev, steps, warmup):
     """Boundary 2: host CSR in -> host CSR out, PCIe-inclusive, through
     rp_project_stream (chunk k+1 uploading while chunk k projects and chunk k-1 downloads). The
     timed region starts with A in host memory and ends with C in host memory. At N ranks every rank
     streams its OWN shard (the recipe's executors, code/clustermode/randomProjection.py:107-113)
     from host memory on its GPU's NUMA node; no collective runs in the loop: a barrier brackets the
-    timed steps and the wall time is the max over ranks."""
+    timed steps and the wall time is the max over ranks. Returns the rank-reduced numbers."""
     import torch
 
     from randomprojection_amd import hostmem
@@ -516,8 +535,6 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
     torch.from_numpy(ap).copy_(Ap.to(torch.int64).to(torch.from_numpy(ap).dtype))
     torch.from_numpy(aj).copy_(Aj)
     torch.from_numpy(ax).copy_(Ax)
-    del Ap, Aj, Ax
-    torch.cuda.empty_cache()
     exp = nnz_a * P.nnz / P.m
     cap = int(1.02 * exp + 8 * np.sqrt(exp)) + 65536
     out = (hm.empty(n + 1, np.int32 if cap < 2**31 else np.int64), hm.empty(cap, np.int32), hm.empty(cap, np.float32))
@@ -526,15 +543,15 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
     def step():
         return P.project_stream(ap, aj, ax, order=order, chunk_rows=args.chunk_rows, out=out)
 
-    for _ in range(max(args.warmup, 1)):
+    for _ in range(max(warmup, 1)):
         cp, cj, cx = step()
     _barrier(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         cp, cj, cx = step()
     t_wall = time.perf_counter() - t0
     _barrier(dev)
-    dt = _allreduce(t_wall, "max", dev) / args.steps
+    dt = _allreduce(t_wall, "max", dev) / steps
     nnz_c = int(cj.size)
     h2d = ap.nbytes + aj.nbytes + ax.nbytes
     d2h = cp.nbytes + cj.nbytes + cx.nbytes
@@ -552,9 +569,22 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
     C = sp.csr_matrix((cx, cj, cp), shape=(n, args.p))[rows]
     same = (np.array_equal(C.indptr, Wp) and np.array_equal(C.indices, Wj)
             and np.array_equal(C.data.view(np.uint32), Wx.view(np.uint32)))
-    same_all = _allreduce(1.0 if same else 0.0, "min", dev) == 1.0
-    ptr_ok = _allreduce(1.0 if (cp[0] == 0 and int(cp[-1]) == nnz_c) else 0.0, "min", dev) == 1.0
-    nnz_all = _allreduce(float(nnz_c), "max", dev)
+    res = {
+        "dt": dt, "n": n, "nnz_a": nnz_a, "nnz_c": nnz_c, "h2d": h2d, "d2h": d2h, "numa": numa,
+        "sample_rows": int(rows.size),
+        "same": _allreduce(1.0 if same else 0.0, "min", dev) == 1.0,
+        "ptr_ok": _allreduce(1.0 if (cp[0] == 0 and int(cp[-1]) == nnz_c) else 0.0, "min", dev) == 1.0,
+        "nnz_max": int(_allreduce(float(nnz_c), "max", dev)),
+    }
+    del A, C, cp, cj, cx, out, ap, aj, ax
+    hm.free()
+    return res
+
+
+def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
+    """--boundary host: the boundary-2 line on its own (host_stream_leg, args.steps timed passes)."""
+    h = host_stream_leg(args, P, R_host, Ap, Aj, Ax, world, rank, dev, args.steps, args.warmup)
+    dt, n, h2d, d2h = h["dt"], h["n"], h["h2d"], h["d2h"]
     if rank == 0:
         out_line = {
             "metric": "rows/sec projected (whole node), host CSR in -> host CSR out (PCIe-inclusive, chunked row "
@@ -565,25 +595,25 @@ def bench_host(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):
             "config": {"workload": "configs[1] host boundary: " + cfg["workload"].format(rows=n, m=args.m, p=args.p)
                                    .replace("device-resident CSR in/out", "host CSR in/out"),
                        "boundary": "host", "host_mem": args.host_mem, "chunk_rows": args.chunk_rows or 2 << 20,
-                       "rows_per_gpu": n, "nnz_in": nnz_a, "nnz_out": nnz_c, "max_nnz_out_over_ranks": int(nnz_all),
-                       "order": order, "parallelism": f"row-shard x{world}, own shard per rank, no collective in the loop",
-                       "numa_rank0": numa},
+                       "rows_per_gpu": n, "nnz_in": h["nnz_a"], "nnz_out": h["nnz_c"],
+                       "max_nnz_out_over_ranks": h["nnz_max"], "order": args.order,
+                       "parallelism": f"row-shard x{world}, own shard per rank, no collective in the loop",
+                       "numa_rank0": h["numa"]},
             "pcie": {"h2d_bytes_per_gpu": h2d, "d2h_bytes_per_gpu": d2h, "h2d_GBps_per_gpu": h2d / dt / 1e9,
                      "d2h_GBps_per_gpu": d2h / dt / 1e9, "host_dram_GBps_node": (h2d + d2h) * world / dt / 1e9,
-                     "link_peak_GBps_per_direction": 63.0, "measured_copy_GBps": "H2D ~55, D2H 48-55 concurrently "
-                     "(scripts/probes/pcie_probe2.hip)"},
-            "roofline": {"bound": "pcie", "achieved": h2d / dt / 1e9, "peak": 63.0, "unit": "GB/s",
-                         "frac": h2d / dt / 1e9 / 63.0, "traffic": None,
+                     "link_peak_GBps_per_direction": PCIE_PEAK_GBS, "measured_copy_GBps": "H2D ~55, D2H 48-55 "
+                     "concurrently (scripts/probes/pcie_probe2.hip)"},
+            "roofline": {"bound": "pcie", "achieved": h2d / dt / 1e9, "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                         "frac": h2d / dt / 1e9 / PCIE_PEAK_GBS, "traffic": None,
                          "note": "per GPU: the upload direction binds (92 B/row in vs 53 B/row out); kernel "
                                  "roofline: the device-resident line"},
             "cpu_baseline": None,
-            "verified": {"sample_rows_per_rank": int(rows.size), "sample_bitexact_vs_oracle": bool(same_all),
-                         "indptr_ok": bool(ptr_ok)},
+            "verified": {"sample_rows_per_rank": h["sample_rows"], "sample_bitexact_vs_oracle": bool(h["same"]),
+                         "indptr_ok": bool(h["ptr_ok"])},
             "librp": {"build_id": LIB_ID, "checked_against_sources": LIB_CHECKED},
             **args.dist_info,
         }
         print(json.dumps(out_line), flush=True)
-    hm.free()
 
 
 def bench_libsvm(args, cfg, P, R_host, Ap, Aj, Ax, world=1, rank=0, dev=None):

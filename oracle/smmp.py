@@ -25,7 +25,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "liboracle_smmp.so")
+# ORACLE_SMMP_LIB: another build of the same source (tests/sanitize: the ASan/UBSan one)
+_LIB_PATH = os.environ.get("ORACLE_SMMP_LIB") or os.path.join(_HERE, "build", "liboracle_smmp.so")
 _lib = None
 
 

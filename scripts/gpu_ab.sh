@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 for r in $(seq "${ROUNDS:-2}"); do
   for L in "" ${LIBS:-}; do
     arg=""; [ -n "$L" ] && arg="--lib $L"
-    timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline ${BENCH:-} $arg 2>/dev/null \
+    timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --host-steps 0 ${BENCH:-} $arg 2>/dev/null \
       | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('${L:-package}', d['librp']['build_id'], round(d['ms_per_step'], 3), d['verified']['sample_bitexact_vs_oracle'])" \
       || exit 9
   done
