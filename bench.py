@@ -163,6 +163,7 @@ def main():
     ap.add_argument("--host-steps", type=int, default=None,
                     help="device line: timed passes of the boundary-2 leg (host CSR stream) on the same rows "
                          "after the device-resident measurement (default 3 for --config kdd, else 0 = skip)")
+    ap.add_argument("--lpr-chunk-rows", type=int, default=None, help="row-lane rows per chunk (RP_OPT_CHUNK_ROWS)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
@@ -283,6 +284,8 @@ def main():
         P.set_staging(args.staging, args.stage_shift)
     if args.pipeline != "auto":
         P.set_option("pipeline", args.pipeline)
+    if args.lpr_chunk_rows is not None:
+        P.set_option("chunk_rows", args.lpr_chunk_rows)
     try:  # full workspace (deferred tile output + staging); the minimal one if HBM is short
         ws = torch.empty(P.workspace_bytes(args.rows, nnz_a, dtype=Ax.dtype), dtype=torch.uint8, device=dev)
     except torch.OutOfMemoryError:

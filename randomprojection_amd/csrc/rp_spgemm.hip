@@ -1018,7 +1018,13 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
 // slice). The bucket's nonempty-feature bitmap (2^sb bits) is staged in LDS: an entry whose R row
 // is empty (57% of KDD2012 entries) gets D = 0 without an L2 request, the others gather their
 // W32 word. S in, D out: both streamed whole-line.
-constexpr int kGBlock = 512;  // 8 waves share one staged bitmap (64 KB at 2^19 features)
+#ifndef RP_GATHER_BLOCK  // A/B builds (scripts/build_variant.py)
+#define RP_GATHER_BLOCK 512
+#endif
+#ifndef RP_GATHER_U
+#define RP_GATHER_U 8
+#endif
+constexpr int kGBlock = RP_GATHER_BLOCK;  // 8 waves share one staged bitmap (64 KB at 2^19 features)
 __global__ void __launch_bounds__(kGBlock)
 lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__ BM, const int64_t* __restrict__ GB,
                   const uint32_t* __restrict__ FILL, int sb, int nb, unsigned groups, const uint32_t* __restrict__ S,
@@ -1037,7 +1043,7 @@ lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__
     __syncthreads();
     const uint32_t mask = (1u << sb) - 1u;
     const uint32_t wb = b << sb;
-    constexpr int kU = 8;
+    constexpr int kU = RP_GATHER_U;
     // S words streamed (non-temporal: keep the slice in L2), the next chunk's in flight while this
     // chunk's W32 words are gathered
     auto load = [&](uint32_t (&v)[kU], int64_t f0) {
@@ -1171,18 +1177,39 @@ __device__ __forceinline__ bool lpr_bloom(const uint16_t* cb, uint32_t kst, uint
     return hit;
 }
 
-// A wave's slot to HBM as built (row r's kept entries at [kst, kst + kept), in first-touch order,
-// or ascending for RP_ORDER_SORTED; entries the exact path dropped leave gaps): `extent` entries
-// copied coalesced, each row's (kst, kept) in rowmeta, the run's entry count in *cnt. The copy
-// kernel puts each row in its final place and order (reversed for scipy's reverse first-touch
-// order): that per-output row search runs there, in a memory-bound kernel, not here.
+// A wave's slot to HBM (row r's kept entries at [kst, kst + kept), in first-touch order, or
+// ascending for RP_ORDER_SORTED): `extent` entries copied coalesced, each row's (kst, kept) in
+// rowmeta, the run's entry count in *cnt. A slot without gaps (every row with entries starts at
+// the kept count of the rows before it: the usual case) is stored in its final order, each row
+// reversed here for scipy's reverse first-touch order, and the copy kernel moves it as one run;
+// a slot with gaps (entries the exact path merged or dropped) is stored as built, and the copy
+// kernel finds each output's row and reverses it there. Both kernels apply the same test
+// (lpr_slot_final).
+__device__ __forceinline__ bool lpr_slot_final(uint32_t c, uint32_t kst, uint32_t pre) {
+    return __ballot(c > 0 && kst != pre) == 0;
+}
 template <typename T>
-__device__ __forceinline__ void lpr_store_slot(const uint16_t* cb, const T* vb, uint32_t kst, uint32_t kept,
-                                               bool valid, int lane, uint32_t extent,
+__device__ __forceinline__ void lpr_store_slot(uint16_t* cb, T* vb, uint32_t kst, uint32_t kept,
+                                               bool valid, int lane, uint32_t extent, int order,
                                                uint32_t* __restrict__ rowmeta, uint32_t* __restrict__ cnt,
                                                uint16_t* __restrict__ oc, T* __restrict__ ov) {
     const uint32_t c = valid ? kept : 0u;
-    const uint32_t tot = __builtin_amdgcn_readlane(wave_scan_dpp(c), 63);
+    const uint32_t incl = wave_scan_dpp(c);
+    const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+    if (order != RP_ORDER_SORTED && lpr_slot_final(c, kst, incl - c)) {
+        const uint32_t half = c >> 1;
+        for (uint32_t i = 0; __ballot(i < half); ++i)
+            if (i < half) {
+                const uint32_t a = kst + i, b = kst + c - 1 - i;
+                const uint16_t ca = cb[a], cz = cb[b];
+                const T va = vb[a], vz = vb[b];
+                cb[a] = cz;
+                cb[b] = ca;
+                vb[a] = vz;
+                vb[b] = va;
+            }
+        __builtin_amdgcn_wave_barrier();
+    }
     if (valid) rowmeta[lane] = kst | (c << 16);
     if (lane == 0) *cnt = tot;
     for (uint32_t o = lane; o < extent; o += 64) {
@@ -1376,7 +1403,6 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     uint16_t* cb = s_colbuf + (size_t)w * sp.slot;
     T* vb = s_valbuf + (size_t)w * sp.slot;
     uint32_t carry_r = 0, carry_k = 0;
-    const T nmag = -mag;
     auto step = [&](uint32_t j, T x) {
         const uint32_t e = E0 + 64 * j + lane;
         const bool ve = e < E1;
@@ -1386,7 +1412,10 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
         const uint32_t d = ve ? s_desc[e] : 0u;
         const uint32_t n = d >> 30;
         const uint32_t np = n < 3 ? n : (d >> 26) & 15u;  // n == 3: a side entry (count in the word)
-        const bool nzx = tmul<T>(x, mag) != T(0);  // all products of an entry share |x * mag|
+        // all products of an entry are +-(x * mag) (x * -mag is -(x * mag) exactly; a kept product
+        // is nonzero, so scipy's 0 + it is itself)
+        const T xm = tmul<T>(x, mag);
+        const bool nzx = xm != T(0);
         const uint32_t kc = nzx ? np : 0u;
         const uint32_t kinc = wave_scan_dpp(kc);
         const uint32_t K = carry_k + kinc - kc;
@@ -1394,11 +1423,11 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
         const uint32_t sl0 = d & 0x7fffu, sl1 = (d >> 15) & 0x7fffu;
         if (n < 3 && kc >= 1 && K < sp.slot) {
             cb[K] = (uint16_t)(sl0 & 0x3fffu);
-            vb[K] = tadd<T>(T(0), tmul<T>(x, (sl0 & 0x4000u) ? nmag : mag));
+            vb[K] = (sl0 & 0x4000u) ? -xm : xm;
         }
         if (n < 3 && kc >= 2 && K + 1 < sp.slot) {
             cb[K + 1] = (uint16_t)(sl1 & 0x3fffu);
-            vb[K + 1] = tadd<T>(T(0), tmul<T>(x, (sl1 & 0x4000u) ? nmag : mag));
+            vb[K + 1] = (sl1 & 0x4000u) ? -xm : xm;
         }
         // side entries keep a gap [K, K + np) in the slot, filled after the pass (their W words
         // may still be in flight); a zero product is not in the slot: its row takes the exact path
@@ -1559,7 +1588,7 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     }
     __builtin_amdgcn_wave_barrier();
     const size_t wt = (size_t)tile * 4 + w;
-    lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
+    lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, order, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
                       sp.cnt + wt, sp.cols + wt * sp.slot, reinterpret_cast<T*>(sp.vals) + wt * sp.slot);
 }
 
@@ -1628,9 +1657,6 @@ __device__ __forceinline__ uint32_t reg_pick(const uint32_t (&v)[N], uint32_t x)
 constexpr int kWaveUnits = 4 * kPartTiles;
 #ifndef RP_WAVE_UNITS  // A/B builds (scripts/build_variant.py): 1 or kWaveUnits
 #define RP_WAVE_UNITS 1
-#endif
-#ifndef RP_WAVE_NT     // A/B builds: 1 = non-temporal S/D loads
-#define RP_WAVE_NT 0
 #endif
 template <typename T, typename IP, int WU, int WPE = std::is_same<T, float>::value ? 7 : 1>
 __global__ void __launch_bounds__(64 * WU) __attribute__((amdgpu_waves_per_eu(WPE)))
@@ -1744,24 +1770,28 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             return;
         }
         __builtin_amdgcn_wave_barrier();
-        const uint32_t bc = lane < kWaveSteps ? (uint32_t)__popcll(sbm[lane]) : 0u;
-        const uint32_t bpre = wave_scan_dpp(bc) - bc;  // start bits in the bitmap words below `lane`
+        // lane x < kWaveSteps: bitmap word x and the start bits below it (read back per step as
+        // wave-uniform values: position 64 x + lane's run is then two mbcnt instructions away)
+        const uint64_t bw = lane < kWaveSteps ? sbm[lane] : 0ull;
+        const uint32_t bc = (uint32_t)__popcll(bw);
+        const uint32_t bpre = wave_scan_dpp(bc) - bc;
+        const uint32_t bw_lo = (uint32_t)bw, bw_hi = (uint32_t)(bw >> 32);
         const uint32_t* __restrict__ St = stg.s + g0;
         const uint32_t* __restrict__ Dt = stg.d + g0;
         uint32_t sv[kWaveSteps];
-        // plain loads: the neighbouring units of the super-tile read the same lines
+        // plain loads (the neighbouring units of the super-tile read the same lines), 32-bit byte
+        // offsets from the group base (a group's words stay far below 2^30)
         auto sd_load = [&](int x) {
-            const uint32_t p = std::min(64u * x + lane, nu - 1);
-            const uint32_t k = (uint32_t)__shfl((int)bpre, (int)(p >> 6), 64) +
-                               (uint32_t)__popcll(sbm[p >> 6] & (~0ull >> (63 - (p & 63)))) - 1u;
-            const uint32_t i = ksrc[k] + p;
-            if (RP_WAVE_NT) {
-                sv[x] = __builtin_nontemporal_load(St + i);
-                dv[x] = __builtin_nontemporal_load(Dt + i);
-            } else {
-                sv[x] = St[i];
-                dv[x] = Dt[i];
-            }
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)bw_lo, x);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)bw_hi, x);
+            const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)bpre, x);
+            // start bits at positions [0, lane] of word x: bit 0, then bits 1..lane (mbcnt of w >> 1)
+            const uint32_t lo1 = (lo >> 1) | (hi << 31), hi1 = hi >> 1;
+            const uint32_t k = b0 + (lo & 1u) + __builtin_amdgcn_mbcnt_hi(hi1, __builtin_amdgcn_mbcnt_lo(lo1, 0u)) - 1u;
+            const bool in = 64u * x + lane < nu;  // lanes past the unit load the unit's first word
+            const uint32_t i = ksrc[in ? k : 0u] + (in ? 64u * x + lane : 0u);
+            sv[x] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(St) + (i << 2));
+            dv[x] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(Dt) + (i << 2));
         };
 #pragma unroll
         for (int x = 0; x < kW0; ++x) sd_load(x);
@@ -1769,7 +1799,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
 #pragma unroll
             for (int x = kW0; x < kWaveSteps; ++x) sd_load(x);
         }
-        // each D word to its entry's place (lanes past the unit wrote the last word again: skipped)
+        // each D word to its entry's place (lanes past the unit loaded the first word: skipped)
 #pragma unroll
         for (int x = 0; x < kW0; ++x)
             if (64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
@@ -1780,11 +1810,15 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         }
         // the values (after the S/D words: issued earlier they and the S/D words did not fit the
         // register budget together)
+        auto ldx = [&](int x) {  // 32-bit byte offset from the tile's first value
+            return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(Axt) +
+                                               (uint32_t)(std::min(E0 + 64 * x + lane, elast) * sizeof(T)));
+        };
 #pragma unroll
-        for (int x = 0; x < kW0; ++x) xv[x] = Axt[std::min(E0 + 64 * x + lane, elast)];
+        for (int x = 0; x < kW0; ++x) xv[x] = ldx(x);
         if (nsteps > kW0) {  // uniform
 #pragma unroll
-            for (int x = kW0; x < kWaveSteps; ++x) xv[x] = Axt[std::min(E0 + 64 * x + lane, elast)];
+            for (int x = kW0; x < kWaveSteps; ++x) xv[x] = ldx(x);
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -1848,7 +1882,6 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     __builtin_amdgcn_wave_barrier();
     uint32_t carry_r = 0, carry_k = 0, nside = 0;
     bool bad = false;
-    const T nmag = -mag;
     auto step = [&](uint32_t j, uint32_t d, T x) {
         const uint32_t e = E0 + 64 * j + lane;
         const bool ve = e < E1;
@@ -1857,7 +1890,10 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         const uint32_t row = s_nz2row[nr & 63];
         const uint32_t n = d >> 30;
         const uint32_t np = n < 3 ? n : (d >> 26) & 15u;  // code 3: a side entry (count in the word)
-        const bool nzx = tmul<T>(x, mag) != T(0);         // all products of an entry share |x * mag|
+        // all products of an entry are +-(x * mag): x * -mag is -(x * mag) exactly, and a kept
+        // product is nonzero, so 0 + it (scipy's first add) is itself
+        const T xm = tmul<T>(x, mag);
+        const bool nzx = xm != T(0);
         const uint32_t kc = nzx ? np : 0u;
         const uint32_t kinc = wave_scan_dpp(kc);
         const uint32_t K = carry_k + kinc - kc;
@@ -1865,11 +1901,11 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         const uint32_t sl0 = d & 0x7fffu, sl1 = (d >> 15) & 0x7fffu;
         if (n < 3 && kc >= 1 && K < sp.slot) {
             cb[K] = (uint16_t)(sl0 & 0x3fffu);
-            vb[K] = tadd<T>(T(0), tmul<T>(x, (sl0 & 0x4000u) ? nmag : mag));
+            vb[K] = (sl0 & 0x4000u) ? -xm : xm;
         }
         if (n < 3 && kc >= 2 && K + 1 < sp.slot) {
             cb[K + 1] = (uint16_t)(sl1 & 0x3fffu);
-            vb[K + 1] = tadd<T>(T(0), tmul<T>(x, (sl1 & 0x4000u) ? nmag : mag));
+            vb[K + 1] = (sl1 & 0x4000u) ? -xm : xm;
         }
         // side entries keep a gap [K, K + np) in the slot, filled after the pass; a zero product
         // is not in the slot: its row takes the exact path
@@ -2014,7 +2050,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         }
     }
     __builtin_amdgcn_wave_barrier();
-    lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, sp.rowmeta + row0, sp.cnt + rb,
+    lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, order, sp.rowmeta + row0, sp.cnt + rb,
                       sp.cols + (size_t)rb * sp.slot, reinterpret_cast<T*>(sp.vals) + (size_t)rb * sp.slot);
 }
 
@@ -2133,10 +2169,31 @@ lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ 
         if (G + cnt > capacity) continue;
         const uint16_t* __restrict__ sc = sp.cols + wt * sp.slot;
         const T* __restrict__ sv = vals + wt * sp.slot;
+        constexpr int kCopyU = 8;
+        if (lpr_slot_final(kept, kst, pre)) {  // stored in final order (lpr_store_slot): one run
+            for (uint32_t q0 = 0; q0 < cnt; q0 += 64 * kCopyU) {
+                uint16_t cv[kCopyU];
+                T xv[kCopyU];
+#pragma unroll
+                for (int u = 0; u < kCopyU; ++u) {
+                    const uint32_t o = std::min(q0 + 64 * u + lane, cnt - 1);
+                    cv[u] = __builtin_nontemporal_load(sc + o);
+                    xv[u] = __builtin_nontemporal_load(sv + o);
+                }
+#pragma unroll
+                for (int u = 0; u < kCopyU; ++u) {
+                    const uint32_t o = q0 + 64 * u + lane;
+                    if (o < cnt) {
+                        Cj[G + o] = (OI)cv[u];
+                        Cx[G + o] = xv[u];
+                    }
+                }
+            }
+            continue;
+        }
         // the row's first slot entry and the step to the next output: reversed (scipy) or forward
         const bool rev = order != RP_ORDER_SORTED;
         const uint32_t base = rev ? kst + kept - 1 : kst;
-        constexpr int kCopyU = 8;
         for (uint32_t q0 = 0; q0 < cnt; q0 += 64 * kCopyU) {  // wave-uniform trip count
             uint16_t cv[kCopyU];
             T xv[kCopyU];
@@ -3793,6 +3850,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
     if ((c->indptr_type != RP_I32 && c->indptr_type != RP_I64) || (c->indices_type != RP_I32 && c->indices_type != RP_I64))
         return fail(RP_ERR_INVALID, "bad output index types");
     if (a->n_rows < 0 || !a->indptr || !c->indptr) return fail(RP_ERR_INVALID, "bad CSR arrays");
+    if (c->capacity < 0) return fail(RP_ERR_INVALID, "negative output capacity");
     if (c->capacity > 0 && (!c->indices || !c->data)) return fail(RP_ERR_INVALID, "NULL output arrays");
     const int64_t n = a->n_rows;
     int choice = -1;  // staged or direct gathers: sampled on the first chunk, kept for the call
@@ -3966,6 +4024,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
         return fail(RP_ERR_UNSUPPORTED, "libsvm values are float32 (the recipe's astype): R must be float32");
     if ((c->indptr_type != RP_I32 && c->indptr_type != RP_I64) || (c->indices_type != RP_I32 && c->indices_type != RP_I64))
         return fail(RP_ERR_INVALID, "bad output index types");
+    if (c->capacity < 0 || cap_rows < 0) return fail(RP_ERR_INVALID, "negative output capacity");
     if (!c->indptr || (c->capacity > 0 && (!c->indices || !c->data)) || (cap_rows > 0 && !labels))
         return fail(RP_ERR_INVALID, "NULL output arrays");
     if (chunk_bytes <= 0) chunk_bytes = 64ll << 20;
