@@ -415,6 +415,8 @@ def main():
                          "model": "B_row=(4+8a)+a(8+8r)+(4+8c)", "a": a, "r": rbar, "c": c,
                          "traffic_source": f"rocprofv3 FETCH_SIZE x2 (gfx950) + WRITE_SIZE per step, {traffic_file}",
                          "l2_hit_rate_r_gathers": tj_used.get("l2_hit_rate_r_gathers"),
+                         "l2_hit_rate_r_gathers_scope": tj_used.get("l2_hit_rate_r_gathers_scope"),
+                         "l2_hit_rate_gather_kernel": tj_used.get("l2_hit_rate_gather_kernel"),
                          "r_gather_kernel": tj_used.get("gather_kernel"),
                          "l2_hit_rate_main_kernel": tj_used.get("l2_hit_rate_main_kernel"),
                          "pipeline": plan, "librp_src_sha16": LIB_ID,

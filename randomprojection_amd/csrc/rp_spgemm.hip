@@ -99,6 +99,8 @@ struct PackedR {
     const uint64_t* W;
     const uint16_t* O;
     const uint64_t* SW;  // side table: W words of the features with > 2 entries (W32 code 3), or NULL
+    const uint32_t* BM;  // nonempty-feature bitmap (1 bit per feature, m <= 2^26), or NULL
+    uint32_t w_bytes;    // bytes of W when BM is set (the tile kernel's buffer loads)
 };
 constexpr uint64_t kOvf = 7ull << 61;
 constexpr uint32_t kW32J = (1u << 26) - 1;  // side-table index bits of a code-3 W32 word (m <= 2^26)
@@ -497,16 +499,61 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
         T x[kMaxE];
         const int32_t* __restrict__ Ajt = Aj + ea;
         const T* __restrict__ Axt = Ax + ea;
+        bool gated = false;
+        if constexpr (std::is_same<RL, PackedR>::value) gated = R.BM != nullptr && ne > 0;
+        if (gated) {
+            // packed R with a nonempty-feature bitmap (m <= 2^26, L2-resident: 1.25 MB for
+            // configs[3]): an entry whose R row is empty (73% on configs[3]) fetches no W line.
+            // Loads in straight-line rounds (feature ids + values, bitmap words, W words), the W
+            // load of a skipped entry an out-of-range buffer load (returns 0, no memory access)
+            if constexpr (std::is_same<RL, PackedR>::value) {
+                int32_t jv[kMaxE];
 #pragma unroll
-        for (int i = 0; i < kMaxE; ++i) {
-            const uint32_t e = tid + i * kBlock;
-            x[i] = T(0);
-            d[i] = 0;
-            if (e < ne) {
-                uint32_t cnt;
-                x[i] = Axt[e];
-                d[i] = r_describe<T>(R, Ajt[e], cnt);
-                s_eoff[e] = (uint16_t)std::min<uint32_t>(cnt, 0xffffu);
+                for (int i = 0; i < kMaxE; ++i) {
+                    const uint32_t ec = std::min<uint32_t>(tid + i * kBlock, ne - 1);
+                    jv[i] = Ajt[ec];
+                    x[i] = Axt[ec];
+                }
+                uint32_t bw[kMaxE];
+#pragma unroll
+                for (int i = 0; i < kMaxE; ++i) bw[i] = R.BM[(uint32_t)jv[i] >> 5];
+                const __amdgpu_buffer_rsrc_t wr =
+                    __builtin_amdgcn_make_buffer_rsrc((void*)R.W, (short)0, (int)R.w_bytes, 0x00020000);
+#pragma unroll
+                for (int i = 0; i < kMaxE; ++i) {
+                    const uint32_t e = tid + i * kBlock;
+                    const bool take = e < ne && ((bw[i] >> ((uint32_t)jv[i] & 31u)) & 1u);
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b64(wr, take ? (uint32_t)jv[i] << 3 : 0xfffffff8u,
+                                                                        0, 0);
+                    d[i] = ((uint64_t)v[1] << 32) | v[0];
+                    if (e >= ne) x[i] = T(0);
+                }
+#pragma unroll
+                for (int i = 0; i < kMaxE; ++i) {
+                    const uint32_t e = tid + i * kBlock;
+                    if (e < ne) {
+                        uint32_t cnt = (uint32_t)(d[i] >> 61);
+                        if (cnt == 7) {  // long R row (> 4 entries): its record in O
+                            const uint64_t rec = d[i] & kLow61;
+                            cnt = R.O[rec];
+                            d[i] = kOvf | (rec + 1);
+                        }
+                        s_eoff[e] = (uint16_t)cnt;
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < kMaxE; ++i) {
+                const uint32_t e = tid + i * kBlock;
+                x[i] = T(0);
+                d[i] = 0;
+                if (e < ne) {
+                    uint32_t cnt;
+                    x[i] = Axt[e];
+                    d[i] = r_describe<T>(R, Ajt[e], cnt);
+                    s_eoff[e] = (uint16_t)std::min<uint32_t>(cnt, 0xffffu);
+                }
             }
         }
         __syncthreads();
@@ -2897,7 +2944,8 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
         return RP_OK;
     }
     if (h->layout == RP_LAYOUT_PACKED) {
-        PackedR R{(const uint64_t*)h->W.p, (const uint16_t*)h->O.p, (const uint64_t*)h->SW.p};
+        PackedR R{(const uint64_t*)h->W.p, (const uint16_t*)h->O.p, (const uint64_t*)h->SW.p,
+                  (const uint32_t*)h->BM.p, h->BM.p ? (uint32_t)(8 * h->m) : 0u};
         rc = a->data_type == RP_F64
                  ? dispatch_idx<double, PackedR>(R, h->mag, h, a, c, order, ws, n_tiles, plan, lds, st, choice)
                  : dispatch_idx<float, PackedR>(R, (float)h->mag, h, a, c, order, ws, n_tiles, plan, lds, st, choice);

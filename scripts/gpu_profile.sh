@@ -22,5 +22,10 @@ for pmc in "${GS[@]}"; do
   name=$(echo $pmc | tr ' ' '_')
   run timeout -s KILL 300 rocprofv3 --pmc $pmc -T --output-format csv -d gpurun_out/prof_${TAG}_pmc_$name -o pmc -- python3 bench.py $PA > gpurun_out/prof_${TAG}_pmc_$name.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_pmc_$name.log; exit 6; }
 done
-python3 scripts/summarize_profile.py --tag $TAG ${SUM_ARGS:-} --bench-json gpurun_out/prof_${TAG}_bench.json > gpurun_out/summary_$TAG.json && tail -30 gpurun_out/summary_$TAG.json
+PROBE=""
+if [ -n "${PROBE_LIB:-}" ]; then  # the gather probe build: one L2 pass (the W32 lookups' own hit rate)
+  run timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -T --output-format csv -d gpurun_out/prof_${TAG}_probe -o pmc -- python3 bench.py $PA --lib $PROBE_LIB > gpurun_out/prof_${TAG}_probe.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_probe.log; exit 7; }
+  PROBE="--probe-pmc gpurun_out/prof_${TAG}_probe"
+fi
+python3 scripts/summarize_profile.py --tag $TAG ${SUM_ARGS:-} $PROBE --bench-json gpurun_out/prof_${TAG}_bench.json > gpurun_out/summary_$TAG.json && tail -30 gpurun_out/summary_$TAG.json
 exit 0

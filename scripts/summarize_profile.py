@@ -74,6 +74,9 @@ def main():
     ap.add_argument("--bench-json", default=None, help="the bench.py line of the profiled command (pipeline, "
                                                         "librp source hash)")
     ap.add_argument("--no-latest", action="store_true", help="do not overwrite profiles/traffic_latest.json")
+    ap.add_argument("--probe-pmc", default=None,
+                    help="TCC_HIT/TCC_MISS pass of the gather probe build (scripts/probes/make_gather_probe.py: the "
+                         "gather kernel without its W32 loads): the W32 lookups' own L2 hit rate is the difference")
     args = ap.parse_args()
     bench = {}
     if args.bench_json:
@@ -113,6 +116,20 @@ def main():
     # the kernel that gathers R's descriptors: the staged gather when it ran, else the main kernel
     gk = summary["kernels"].get("lpr_gather_kernel", {})
     gather_k = "lpr_gather_kernel" if gk.get("avg_ms", 0) > 0.05 else main_k
+    # the R gathers' own L2 hit rate: the staged gather kernel's requests minus those of its probe
+    # build (same S/D streams, no W32 loads); without a probe, the whole kernel's (streams included)
+    gc = summary["kernels"].get(gather_k, {}).get("counters_per_launch", {})
+    r_hit, r_scope = summary["kernels"].get(gather_k, {}).get("l2_hit_rate"), "whole gather kernel (S/D streams included)"
+    if args.probe_pmc and gather_k == "lpr_gather_kernel" and "TCC_HIT_sum" in gc:
+        pc = pmc_means(args.probe_pmc).get("lpr_gather_kernel", {})
+        if "TCC_HIT_sum" in pc and "TCC_MISS_sum" in pc:
+            dh = gc["TCC_HIT_sum"] - pc["TCC_HIT_sum"]
+            dr = gc["TCC_HIT_sum"] + gc["TCC_MISS_sum"] - pc["TCC_HIT_sum"] - pc["TCC_MISS_sum"]
+            if dr > 0:
+                r_hit, r_scope = dh / dr, "W32 lookups only (gather kernel minus its probe build without them)"
+                summary["r_gathers"] = {"l2_requests_per_launch": dr, "l2_hits_per_launch": dh, "l2_hit_rate": r_hit,
+                                        "probe_counters": pc}
+                json.dump(summary, open(os.path.join(prof, f"{args.tag}_summary.json"), "w"), indent=1)
     if "hbm_bytes" in summary["step"]:
         tj = {"tag": args.tag, "rows": args.rows, "dist": args.dist,
               "pipeline": plan.get("pipeline"), "staged": plan.get("staged"), "src_sha16": roof.get("librp_src_sha16"),
@@ -121,7 +138,9 @@ def main():
               "main_kernel": main_k,
               "l2_hit_rate_main_kernel": summary["kernels"].get(main_k, {}).get("l2_hit_rate"),
               "gather_kernel": gather_k,
-              "l2_hit_rate_r_gathers": summary["kernels"].get(gather_k, {}).get("l2_hit_rate"),
+              "l2_hit_rate_r_gathers": r_hit,
+              "l2_hit_rate_r_gathers_scope": r_scope,
+              "l2_hit_rate_gather_kernel": summary["kernels"].get(gather_k, {}).get("l2_hit_rate"),
               "gather_kernel_read_requests_G_per_s": summary["kernels"].get(gather_k, {}).get("read_requests_G_per_s"),
               "main_kernel_read_requests_per_launch": summary["kernels"].get(main_k, {}).get("read_requests"),
               "l2_hit_rate_step": summary["step"].get("l2_hit_rate"),
