@@ -148,6 +148,19 @@ __device__ __forceinline__ float tadd<float>(float a, float b) { return __fadd_r
 template <>
 __device__ __forceinline__ double tadd<double>(double a, double b) { return __dadd_rn(a, b); }
 
+// one T from a raw buffer (out-of-range offsets read 0 without a memory access)
+template <typename T>
+__device__ __forceinline__ T buf_load_t(__amdgpu_buffer_rsrc_t r, uint32_t off);
+template <>
+__device__ __forceinline__ float buf_load_t<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+template <>
+__device__ __forceinline__ double buf_load_t<double>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return __longlong_as_double((long long)(((uint64_t)v[1] << 32) | v[0]));
+}
+
 // t-th product (column, x * value) of an entry described by d
 template <typename T>
 __device__ __forceinline__ void r_product(const PackedR& R, T mag, uint64_t d, uint32_t t, T x,
@@ -1665,7 +1678,8 @@ constexpr int kWaveScr = 128;                  // exact-path scratch (products o
 // columns + values (every descriptor is in registers before the first slot store); region B = the
 // run lookup (start bitmap, run offsets), later the exact-path scratch
 __host__ __device__ inline size_t lpr_wave_region_a(uint32_t slot, size_t vs, uint32_t ucap) {
-    const size_t s = ((2 * (size_t)slot + 15) & ~size_t(15)) + ((vs * (size_t)slot + 15) & ~size_t(15));
+    // (+2: the flat pass's clamped product stores past a full slot)
+    const size_t s = ((2 * ((size_t)slot + 2) + 15) & ~size_t(15)) + ((vs * ((size_t)slot + 2) + 15) & ~size_t(15));
     return std::max(s, 4 * (size_t)ucap);
 }
 __host__ __device__ inline size_t lpr_wave_lds_bytes(uint32_t slot, size_t vs, uint32_t ucap, int nb) {
@@ -1857,10 +1871,11 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         }
         // the values (after the S/D words: issued earlier they and the S/D words did not fit the
         // register budget together)
-        auto ldx = [&](int x) {  // 32-bit byte offset from the tile's first value
-            return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(Axt) +
-                                               (uint32_t)(std::min(E0 + 64 * x + lane, elast) * sizeof(T)));
-        };
+        // the unit's values as a buffer of nu entries: no clamp (a lane past the unit reads 0, no
+        // memory access), the step offset folds into the instruction
+        const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(Axt + E0), (short)0, (int)(nu * sizeof(T)), 0x00020000);
+        auto ldx = [&](int x) { return buf_load_t<T>(xr, (uint32_t)((64 * x + lane) * sizeof(T))); };
 #pragma unroll
         for (int x = 0; x < kW0; ++x) xv[x] = ldx(x);
         if (nsteps > kW0) {  // uniform
@@ -1870,7 +1885,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int x = 0; x < kWaveSteps; ++x) {
-            const uint32_t v = desc[std::min(64u * x + lane, nu - 1)];
+            const uint32_t v = desc[64u * x + lane];  // (past the unit: any LDS word, masked below)
             dv[x] = 64u * x + lane < nu ? v : 0u;
         }
         // every descriptor is in registers before the slot (region A) is written below
@@ -1901,7 +1916,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             const bool side = (dv[x] >> 30) == 3u && 64u * x + lane < nu;
             const uint64_t sm = __ballot(side);
             if (side) {
-                const uint32_t k = nside_pre + (uint32_t)__popcll(sm & ((1ull << lane) - 1ull));
+                const uint32_t k = nside_pre + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
                 if (k < (uint32_t)kWaveSide) s_sfj[k] = dv[x] & kW32J;
             }
             nside_pre += (uint32_t)__popcll(sm);
@@ -1914,7 +1929,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     const bool valid = lane < nrows;
     const bool nonempty = valid && rend > rs;
     uint16_t* cb = reinterpret_cast<uint16_t*>(lds);
-    T* vb = reinterpret_cast<T*>(lds + ((2 * (size_t)sp.slot + 15) & ~size_t(15)));
+    T* vb = reinterpret_cast<T*>(lds + ((2 * ((size_t)sp.slot + 2) + 15) & ~size_t(15)));
     uint16_t* scol = reinterpret_cast<uint16_t*>(lds + ra);
     T* sval = reinterpret_cast<T*>(lds + ra + ((2 * (size_t)kWaveScr + 15) & ~size_t(15)));
     if ((uint32_t)lane < nsteps) s_flag[lane] = 0ull;
@@ -1945,21 +1960,25 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         const uint32_t kinc = wave_scan_dpp(kc);
         const uint32_t K = carry_k + kinc - kc;
         if (ve && ((fw >> lane) & 1ull)) s_kst[row] = (uint16_t)K;  // the row's first entry
-        const uint32_t sl0 = d & 0x7fffu, sl1 = (d >> 15) & 0x7fffu;
-        if (n < 3 && kc >= 1 && K < sp.slot) {
-            cb[K] = (uint16_t)(sl0 & 0x3fffu);
-            vb[K] = (sl0 & 0x4000u) ? -xm : xm;
-        }
-        if (n < 3 && kc >= 2 && K + 1 < sp.slot) {
-            cb[K + 1] = (uint16_t)(sl1 & 0x3fffu);
-            vb[K + 1] = (sl1 & 0x4000u) ? -xm : xm;
+        // products at K, K + 1 (K clamped: past the slot, both land in its two spare entries; the
+        // unit then goes heavy)
+        const uint32_t Kc = std::min(K, sp.slot);
+        uint16_t* cK = cb + Kc;
+        T* vK = vb + Kc;
+        if (n < 3 && kc >= 1) {
+            cK[0] = (uint16_t)(d & 0x3fffu);
+            vK[0] = (d & 0x4000u) ? -xm : xm;
+            if (kc >= 2) {
+                cK[1] = (uint16_t)((d >> 15) & 0x3fffu);
+                vK[1] = (d & 0x20000000u) ? -xm : xm;
+            }
         }
         // side entries keep a gap [K, K + np) in the slot, filled after the pass; a zero product
         // is not in the slot: its row takes the exact path
         const bool side = ve && n == 3;
         const uint64_t sm = __ballot(side);
         if (side) {
-            const uint32_t k = nside + (uint32_t)__builtin_popcountll(sm & ((1ull << lane) - 1));
+            const uint32_t k = nside + __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
             if (k < (uint32_t)kWaveSide) {  // (its side-table index: listed before the pass)
                 s_sfk[k] = kc ? (uint16_t)K : (uint16_t)0xffffu;
                 s_sfx[k] = x;
