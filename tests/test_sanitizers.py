@@ -134,8 +134,16 @@ def test_host_code_under_asan_ubsan(asan_libs, golden, tmp_path):
         assert same_bits(got[f"oracle/{name}/data"], golden[f"C_{name}_data"])
 
 
+@pytest.fixture(scope="module")
+def ubsan_lib():
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        pytest.skip("no hipcc in this image")
+    subprocess.run(["make", "-s", "-j3", "-C", SAN, "_build/librp_ubsan.so"], check=True, stdout=subprocess.DEVNULL)
+    return os.path.join(BUILD, "librp_ubsan.so")
+
+
 @pytest.mark.gpu
-def test_host_paths_under_ubsan_on_gpu(asan_libs, golden, tmp_path):
+def test_host_paths_under_ubsan_on_gpu(ubsan_lib, golden, tmp_path):
     """On the GPU box, the host code under UBSan (the ASan allocator could not map its heap beside the
     HIP runtime there: 'AddressSanitizer: out of memory' on a 4 MB runtime allocation, so ASan
     covers the host paths the CPU can reach, above) through the projector upload, the host-buffer
@@ -150,7 +158,7 @@ def test_host_paths_under_ubsan_on_gpu(asan_libs, golden, tmp_path):
     if rt is None:
         pytest.skip("no UBSan runtime in this image")
     np.savez(tmp_path / "cases.npz", none=np.zeros(1))
-    r = subprocess.run([sys.executable, "-u", os.path.join(SAN, "asan_driver.py"), os.path.join(BUILD, "librp_ubsan.so"),
+    r = subprocess.run([sys.executable, "-u", os.path.join(SAN, "asan_driver.py"), ubsan_lib,
                         str(tmp_path / "cases.npz"), str(tmp_path / "out.npz"), "gpu"],
                        env=_env(rt), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
