@@ -119,7 +119,9 @@ def main():
     # the R gathers' own L2 hit rate: the staged gather kernel's requests minus those of its probe
     # build (same S/D streams, no W32 loads); without a probe, the whole kernel's (streams included)
     gc = summary["kernels"].get(gather_k, {}).get("counters_per_launch", {})
-    r_hit, r_scope = summary["kernels"].get(gather_k, {}).get("l2_hit_rate"), "whole gather kernel (S/D streams included)"
+    r_hit = summary["kernels"].get(gather_k, {}).get("l2_hit_rate")
+    r_scope = ("whole gather kernel (S/D streams included)" if gather_k == "lpr_gather_kernel"
+               else "whole main kernel (A and C streams included: R is gathered inside it)")
     if args.probe_pmc and gather_k == "lpr_gather_kernel" and "TCC_HIT_sum" in gc:
         pc = pmc_means(args.probe_pmc).get("lpr_gather_kernel", {})
         if "TCC_HIT_sum" in pc and "TCC_MISS_sum" in pc:
