@@ -59,3 +59,26 @@ def test_longrow_deferral(polls):
     P = Projector(R)
     P.set_option("defer_polls", int(polls))
     _check(P, A, R)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_longrow_bitmap_gated_gathers(dtype):
+    """The tile kernel fetches W words only for features whose R row is nonempty (feature bitmap;
+    skipped entries read an out-of-range buffer offset): m not a multiple of 32, the last features
+    nonempty, 70% empty R rows, rows of more than 4 entries (O records) next to empty ones."""
+    rng = np.random.default_rng(123)
+    m, p = (1 << 20) + 7, 1024
+    live = np.sort(np.concatenate([rng.choice(m - 8, size=int(0.3 * m), replace=False), [m - 3, m - 2, m - 1]]))
+    cnt = rng.choice([1, 1, 1, 2, 2, 3, 6], size=live.size)
+    rows = np.repeat(live, cnt)
+    cols = np.concatenate([np.sort(rng.choice(p, size=k, replace=False)) for k in cnt])
+    mag = 1.5
+    vals = np.where(rng.random(rows.size) < 0.5, -mag, mag).astype(dtype)
+    R = sp.csr_matrix((vals, (rows, cols)), shape=(m, p))
+    A = kdd_like(rng, 4000, m, mean=99, values="normal", dtype=dtype)
+    tail = sp.csr_matrix((np.ones(3, dtype), (np.zeros(3, int), [m - 3, m - 2, m - 1])), shape=(1, m))
+    A = sp.vstack([A, tail, A[:100]]).tocsr()
+    P = Projector(R)
+    assert P.layout == "packed"
+    assert P.plan(A.shape[0], A.nnz)["pipeline"] == "tile"
+    _check(P, A, R)
