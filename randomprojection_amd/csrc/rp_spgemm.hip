@@ -1078,13 +1078,9 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
 // slice). The bucket's nonempty-feature bitmap (2^sb bits) is staged in LDS: an entry whose R row
 // is empty (57% of KDD2012 entries) gets D = 0 without an L2 request, the others gather their
 // W32 word. S in, D out: both streamed whole-line.
-#ifndef RP_GATHER_BLOCK  // A/B builds (scripts/build_variant.py)
-#define RP_GATHER_BLOCK 512
-#endif
-#ifndef RP_GATHER_U
-#define RP_GATHER_U 8
-#endif
-constexpr int kGBlock = RP_GATHER_BLOCK;  // 8 waves share one staged bitmap (64 KB at 2^19 features)
+// 8 waves share one staged bitmap (64 KB at 2^19 features); 1024- or 256-thread workgroups and 4 or
+// 16 entries per thread per round measured slower (§3d)
+constexpr int kGBlock = 512;
 __global__ void __launch_bounds__(kGBlock)
 lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__ BM, const int64_t* __restrict__ GB,
                   const uint32_t* __restrict__ FILL, int sb, int nb, unsigned groups, const uint32_t* __restrict__ S,
@@ -1103,7 +1099,7 @@ lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__
     __syncthreads();
     const uint32_t mask = (1u << sb) - 1u;
     const uint32_t wb = b << sb;
-    constexpr int kU = RP_GATHER_U;
+    constexpr int kU = 8;
     // S words streamed (non-temporal: keep the slice in L2), the next chunk's in flight while this
     // chunk's W32 words are gathered
     auto load = [&](uint32_t (&v)[kU], int64_t f0) {
@@ -1710,41 +1706,26 @@ __device__ __forceinline__ uint32_t reg_pick(const uint32_t (&v)[N], uint32_t x)
     return r;
 }
 // f32: built for 7 waves per SIMD (72 VGPRs: the S/D words and the values in flight together; LDS
-// allows ~29 one-wave workgroups per CU anyway); f64 unconstrained.
-// WU waves per workgroup, each its own unit, no block barrier: WU = 4 kPartTiles puts a super-tile's
-// units on one CU at the same time, so the lines their parts of a run share are fetched once (one
-// wave per workgroup measured 31.4 GB of HBM reads per configs[1] pass: units of one super-tile ran
-// microseconds apart and ~9 MB of run lines per XCD were in flight against a 4 MB L2).
-constexpr int kWaveUnits = 4 * kPartTiles;
-#ifndef RP_WAVE_UNITS  // A/B builds (scripts/build_variant.py): 1 or kWaveUnits
-#define RP_WAVE_UNITS 1
-#endif
-template <typename T, typename IP, int WU, int WPE = std::is_same<T, float>::value ? 7 : 1>
-__global__ void __launch_bounds__(64 * WU) __attribute__((amdgpu_waves_per_eu(WPE)))
+// allows ~29 one-wave workgroups per CU anyway; 8 waves in 64 VGPRs measured slower, §3d); f64
+// unconstrained. One wave per workgroup, each its own unit, no block barrier (a super-tile's 8 units
+// in one workgroup measured slower too: 25.6 vs 18.3 ms, §3d).
+template <typename T, typename IP, int WPE = std::is_same<T, float>::value ? 7 : 1>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
                 const T* __restrict__ Ax, LprStage stg, int cap_a, uint32_t ucap, unsigned n_tiles, unsigned s8,
                 int order, LprSpace sp, Workspace* ws) {
-    extern __shared__ __align__(16) unsigned char lds_all[];  // per wave: region A (descriptors, then slot), B
-    __shared__ uint64_t s_flag_[WU][kWaveSteps];               // row-start bitmap over the unit's entries
-    __shared__ uint64_t s_susp_[WU];                           // rows flagged for the exact path
-    __shared__ uint16_t s_kst_[WU][64];
-    __shared__ uint8_t s_nz2row_[WU][64];
-    __shared__ uint16_t s_sfk_[WU][kWaveSide];                 // side entry's slot position (0xffff: zero x)
-    __shared__ T s_sfx_[WU][kWaveSide];                        // ... its value
-    __shared__ uint32_t s_sfj_[WU][kWaveSide];                 // ... its side-table index
-    const int wv = WU > 1 ? (int)(threadIdx.x >> 6) : 0, lane = threadIdx.x & 63;
-    uint64_t* s_flag = s_flag_[wv];
-    uint64_t& s_susp = s_susp_[wv];
-    uint16_t* s_kst = s_kst_[wv];
-    uint8_t* s_nz2row = s_nz2row_[wv];
-    uint16_t* s_sfk = s_sfk_[wv];
-    T* s_sfx = s_sfx_[wv];
-    uint32_t* s_sfj = s_sfj_[wv];
-    unsigned char* lds = lds_all + (size_t)wv * lpr_wave_lds_bytes(sp.slot, sizeof(T), ucap, stg.nb);
+    extern __shared__ __align__(16) unsigned char lds[];  // region A (descriptors, then slot), region B
+    __shared__ uint64_t s_flag[kWaveSteps];               // row-start bitmap over the unit's entries
+    __shared__ uint64_t s_susp;                           // rows flagged for the exact path
+    __shared__ uint16_t s_kst[64];
+    __shared__ uint8_t s_nz2row[64];
+    __shared__ uint16_t s_sfk[kWaveSide];                 // side entry's slot position (0xffff: zero x)
+    __shared__ T s_sfx[kWaveSide];                        // ... its value
+    __shared__ uint32_t s_sfj[kWaveSide];                 // ... its side-table index
+    const int lane = threadIdx.x & 63;
     // unit order follows the partition's XCD ranges: XCD x takes the units of super-tiles
     // [x * s8, (x + 1) * s8) in order (workgroup i runs on XCD i % 8)
-    const unsigned rb = WU > 1 ? xcd_tile(blockIdx.x, s8) * WU + wv
-                               : (blockIdx.x & 7u) * (4u * kPartTiles * s8) + (blockIdx.x >> 3);
+    const unsigned rb = (blockIdx.x & 7u) * (4u * kPartTiles * s8) + (blockIdx.x >> 3);
     if (rb >= 4 * n_tiles) return;
     const unsigned tile = rb >> 2, u = rb & 3;
     const int64_t row0 = (int64_t)rb * 64;
@@ -2772,11 +2753,10 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
                            pl.groups, (const uint32_t*)Sw, Dw, gate);
         HIP_TRY(hipGetLastError());
         const LprStage stg{gate, (const uint32_t*)h->W32.p, OFF2, CU, GB, Sw, Dw, pl.ostride, pl.nb};
-        constexpr int WU = RP_WAVE_UNITS;
-        const size_t wlds = WU * lpr_wave_lds_bytes(pl.lpr_slot, sizeof(T), pl.ucap, pl.nb);
-        HIP_TRY(hipFuncSetAttribute((const void*)lpr_wave_kernel<T, IP, WU>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)wlds));
-        hipLaunchKernelGGL((lpr_wave_kernel<T, IP, WU>), dim3(8u * (4u * kPartTiles / WU) * s8), dim3(64 * WU), wlds,
+        const size_t wlds = lpr_wave_lds_bytes(pl.lpr_slot, sizeof(T), pl.ucap, pl.nb);
+        HIP_TRY(hipFuncSetAttribute((const void*)lpr_wave_kernel<T, IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)wlds));
+        hipLaunchKernelGGL((lpr_wave_kernel<T, IP>), dim3(8u * 4u * kPartTiles * s8), dim3(64), wlds,
                            st, R, mag, a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, pl.ucap, n_tiles, s8, order,
                            sp, ws);
     } else {
