@@ -143,6 +143,10 @@ def test_bench_gpus_two_launches_two_ranks():
     assert v["sample_bitexact_vs_oracle"] and v["indptr_ok"] and v["columns_ok"] and v["ranks_verified"] == 2
     assert line["cpu_baseline"] and line["cpu_baseline"]["value"] > 0
     assert line["librp"]["checked_against_sources"] and line["value"] > 0
+    # boundary 2 beside it: every rank streams its own rows host CSR -> host CSR, checked after the clock
+    h = line["boundaries"]["host"]
+    assert h["rows_per_s"] > 0 and h["verified"]["sample_bitexact_vs_oracle"] and h["verified"]["indptr_ok"]
+    assert h["verified"]["nnz_out_equal_device_leg"]
 
 
 def test_bench_rccl_path_one_rank():
