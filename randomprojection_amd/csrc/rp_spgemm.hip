@@ -1558,21 +1558,28 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     uint32_t kept = nonempty ? kend - kst : 0u;
     bool hit = false;
     if (!overflow) hit = lpr_bloom(cb, kst, kept);
-    uint64_t todo = s_susp[w] | __ballot(hit);  // lane == row within the wave
+    const uint64_t susp = s_susp[w];
+    uint64_t todo = susp | __ballot(hit);  // lane == row within the wave
     __builtin_amdgcn_wave_barrier();  // the row-start bitmap is dead from here: the scratch reuses it
     constexpr int kScr = (int)((kLprFlagWords * 8 - 16) / (2 + sizeof(T)));
     uint16_t* scol = reinterpret_cast<uint16_t*>(&s_flag[w][0]);
     T* sval = reinterpret_cast<T*>(reinterpret_cast<unsigned char*>(&s_flag[w][0]) + ((2 * kScr + 15) & ~15));
     if (__ballot(overflow)) todo = 0;
-    // exact path, one flagged row at a time, the whole wave on it: its products in sequence order
-    // into the scratch, then every product checks for an earlier one of its column (first touch);
-    // a leader sums its group in order; kept leaders land in the row's slot range in that order
+    // exact path, one flagged row at a time, the whole wave on it: its products in sequence order,
+    // then every product checks for an earlier one of its column (first touch); a leader sums its
+    // group in order; kept leaders land in the row's slot range in that order. A Bloom-flagged row
+    // is read from its slot range (64 products or fewer: one round, reads before writes); a row
+    // with a zero value rebuilds its products into the scratch (as lpr_wave_kernel)
     while (todo) {
         const int R0 = __builtin_ctzll(todo);
         todo &= todo - 1;
         const uint32_t a0 = __shfl(rs, R0, 64), a1 = __shfl(re, R0, 64), kR = __shfl(kst, R0, 64);
-        uint32_t nprod = 0;
-        for (uint32_t e0 = a0; e0 < a1; e0 += 64) {
+        const uint32_t kE = __shfl(kend, R0, 64);
+        const bool from_slot = !((susp >> R0) & 1ull) && kE - kR <= 64u;  // uniform
+        const uint16_t* pc = from_slot ? cb + kR : scol;
+        const T* pv = from_slot ? vb + kR : sval;
+        uint32_t nprod = from_slot ? kE - kR : 0u;
+        for (uint32_t e0 = a0; !from_slot && e0 < a1; e0 += 64) {
             const uint32_t e = e0 + lane;
             const bool in = e < a1;
             const uint32_t d = in ? s_desc[e] : 0u;
@@ -1598,13 +1605,14 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
             const uint32_t q = q0 + lane;
             bool lead = q < nprod;
             T sum = T(0);
+            uint16_t cq = 0;
             if (lead) {
-                const uint16_t cq = scol[q];
-                for (uint32_t b = 0; b < q && lead; ++b) lead = scol[b] != cq;
+                cq = pc[q];
+                for (uint32_t b = 0; b < q && lead; ++b) lead = pc[b] != cq;
                 if (lead) {
-                    sum = tadd<T>(T(0), sval[q]);
+                    sum = tadd<T>(T(0), pv[q]);
                     for (uint32_t b = q + 1; b < nprod; ++b)
-                        if (scol[b] == cq) sum = tadd<T>(sum, sval[b]);
+                        if (pc[b] == cq) sum = tadd<T>(sum, pv[b]);
                 }
             }
             const bool keep = lead && sum != T(0);
@@ -1612,7 +1620,7 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
             if (keep) {
                 if (kR + nk + ki - 1 >= sp.slot) overflow = true;
                 else {
-                    cb[kR + nk + ki - 1] = scol[q];
+                    cb[kR + nk + ki - 1] = cq;
                     vb[kR + nk + ki - 1] = sum;
                 }
             }
@@ -2011,18 +2019,26 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     uint32_t kept = nonempty ? kend_r - kst : 0u;
     bool hit = false;
     if (!overflow) hit = lpr_bloom(cb, kst, kept);
-    uint64_t todo = s_susp | __ballot(hit);  // lane == row within the unit
+    const uint64_t susp = s_susp;
+    uint64_t todo = susp | __ballot(hit);  // lane == row within the unit
     if (__ballot(overflow)) todo = 0;
-    // exact path, one flagged row at a time, the whole wave on it: its products in sequence order
-    // into the scratch, then every product checks for an earlier one of its column (first touch);
-    // a leader sums its group in order; kept leaders land in the row's slot range in that order.
-    // The row's descriptors come from the registers (entry e - E0 = step x, lane l: dv[x] of lane l)
+    // exact path, one flagged row at a time, the whole wave on it: its products in sequence order,
+    // then every product checks for an earlier one of its column (first touch); a leader sums its
+    // group in order; kept leaders land in the row's slot range in that order. A row the Bloom check
+    // flagged already has all its products in sequence order in its slot range: read there (64 or
+    // fewer: one round, every read before the first write). A row with a zero value (its zero
+    // products are not in the slot) rebuilds them into the scratch from the descriptors in the
+    // registers (entry e - E0 = step x, lane l: dv[x] of lane l).
     while (todo) {
         const int R0 = __builtin_ctzll(todo);
         todo &= todo - 1;
         const uint32_t a0 = __shfl(rs, R0, 64), a1 = __shfl(rend, R0, 64), kR = __shfl(kst, R0, 64);
-        uint32_t nprod = 0;
-        for (uint32_t e0 = a0; e0 < a1; e0 += 64) {
+        const uint32_t kE = __shfl(kend_r, R0, 64);
+        const bool from_slot = !((susp >> R0) & 1ull) && kE - kR <= 64u;  // uniform
+        const uint16_t* pc = from_slot ? cb + kR : scol;
+        const T* pv = from_slot ? vb + kR : sval;
+        uint32_t nprod = from_slot ? kE - kR : 0u;
+        for (uint32_t e0 = a0; !from_slot && e0 < a1; e0 += 64) {
             const uint32_t e = e0 + lane;
             const bool in = e < a1;
             // entries [e0, e0 + 64) lie in steps x0 = (e0 - E0) / 64 and x0 + 1
@@ -2052,13 +2068,14 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             const uint32_t q = q0 + lane;
             bool lead = q < nprod;
             T sum = T(0);
+            uint16_t cq = 0;
             if (lead) {
-                const uint16_t cq = scol[q];
-                for (uint32_t b = 0; b < q && lead; ++b) lead = scol[b] != cq;
+                cq = pc[q];
+                for (uint32_t b = 0; b < q && lead; ++b) lead = pc[b] != cq;
                 if (lead) {
-                    sum = tadd<T>(T(0), sval[q]);
+                    sum = tadd<T>(T(0), pv[q]);
                     for (uint32_t b = q + 1; b < nprod; ++b)
-                        if (scol[b] == cq) sum = tadd<T>(sum, sval[b]);
+                        if (pc[b] == cq) sum = tadd<T>(sum, pv[b]);
                 }
             }
             const bool keep = lead && sum != T(0);
@@ -2066,7 +2083,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
             if (keep) {
                 if (kR + nk + ki - 1 >= sp.slot) overflow = true;
                 else {
-                    cb[kR + nk + ki - 1] = scol[q];
+                    cb[kR + nk + ki - 1] = cq;
                     vb[kR + nk + ki - 1] = sum;
                 }
             }
