@@ -101,12 +101,14 @@ def launch_ranks(n: int) -> int:
     return bad[0] if bad else 0
 
 
-def step_kernels(plan, staged_run):
-    """The kernels one rp_project_device call runs for this plan (rp_spgemm.hip). In auto mode the
-    host reads lpr_choose_kernel's verdict and launches only the chosen branch."""
+def step_kernels(plan, staged_run, call="sync"):
+    """The kernels one rp_project_device call runs for this plan (rp_spgemm.hip). In auto mode a
+    sync call has the host read lpr_choose_kernel's verdict and launch only the chosen branch; an
+    async one launches the staged branch, gated on the device by the verdict."""
     if plan["pipeline"] == "rowlane":
+        staged_kernels = staged_run or (call == "async" and plan["staged"] == "auto")
         main = ["lpr_reserve_kernel", "lpr_partition_kernel", "lpr_gather_kernel",
-                "lpr_wave_kernel"] if staged_run else ["lpr_main_flat_kernel"]
+                "lpr_wave_kernel"] if staged_kernels else ["lpr_main_flat_kernel"]
         ks = main + ["lpr_heavy_count_kernel", "lpr_scan_kernel", "lpr_copy_kernel", "lpr_heavy_write_kernel"]
         if plan["staged"] == "auto":
             ks = ["lpr_choose_kernel"] + ks
@@ -164,6 +166,11 @@ def main():
                     help="device line: timed passes of the boundary-2 leg (host CSR stream) on the same rows "
                          "after the device-resident measurement (default 3 for --config kdd, else 0 = skip)")
     ap.add_argument("--lpr-chunk-rows", type=int, default=None, help="row-lane rows per chunk (RP_OPT_CHUNK_ROWS)")
+    ap.add_argument("--call", choices=["sync", "async"], default="sync",
+                    help="sync: each step asks for the exact nnz (rp_project_device with total_nnz: the host "
+                         "reads the staging verdict and launches only the chosen branch, then waits for the "
+                         "result); async: total_nnz NULL (never waits on the host; the verdict gates the staged "
+                         "kernels on the device)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     args = ap.parse_args()
     env_world = os.environ.get("WORLD_SIZE")
@@ -312,7 +319,10 @@ def main():
     log(f"[rank {rank}] pipeline: {plan}")
 
     def step():
-        P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=args.order, stream=stream, workspace=ws, nnz_a=nnz_a, sync=False)
+        k = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, order=args.order, stream=stream, workspace=ws, nnz_a=nnz_a,
+                             sync=args.call == "sync")
+        if k is not None and k != nnz_c:
+            raise RuntimeError(f"step nnz {k} != first run's {nnz_c}")
 
     for _ in range(args.warmup):
         step()
@@ -408,7 +418,8 @@ def main():
             "data": cfg["data"].format(dist=args.dist, p=args.p),
             "config": {"workload": cfg["workload"].format(rows=args.rows, m=args.m, p=args.p),
                        "rows_per_gpu": args.rows, "m": args.m, "p": args.p, "nnz_in": nnz_a, "nnz_out": nnz_c,
-                       "order": args.order, "r_layout": P.layout, "parallelism": f"row-shard x{world}"},
+                       "order": args.order, "r_layout": P.layout, "parallelism": f"row-shard x{world}",
+                       "call": args.call},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kernel_ms, "bytes_per_row": b_row,
@@ -420,7 +431,7 @@ def main():
                          "r_gather_kernel": tj_used.get("gather_kernel"),
                          "l2_hit_rate_main_kernel": tj_used.get("l2_hit_rate_main_kernel"),
                          "pipeline": plan, "librp_src_sha16": LIB_ID,
-                         "step_kernels": step_kernels(plan, staged_run),
+                         "step_kernels": step_kernels(plan, staged_run, args.call),
                          "traffic_GBps": (traffic / (kernel_ms * 1e-3) / 1e9) if traffic else None,
                          "random_line_ceiling_G_per_s": RANDOM_LINE_CEILING / 1e9,
                          "r_gather_kernel_line_requests_G_per_s": req,

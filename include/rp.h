@@ -19,8 +19,8 @@
  *      projected_features = features_matrix.dot(local_csr_matrix)
  *                                                        code/clustermode/randomProjection.py:46
  *      -> scipy _sparsetools.csr_matmat_maxnnz + csr_matmat  scipy/sparse/_compressed.py:569-595
- *    Device-resident CSR in, device-resident CSR out, asynchronous on one stream (in auto staging
- *    mode the host reads a 4-byte verdict of a sampling kernel first). The call runs one of the
+ *    Device-resident CSR in, device-resident CSR out, asynchronous on one stream (when the caller
+ *    asks for the nnz, the host also reads a 4-byte verdict of a sampling kernel first). The call runs one of the
  *    kernel pipelines rp_project_plan reports: the row-lane pipeline for short rows over a packed R
  *    (KDD2012: staging choice, then either segment reserves, super-tile partition, bitmap-filtered
  *    gather and the wave kernel, or the direct main kernel; heavy-tile count/write, scan, copy), or
@@ -122,8 +122,15 @@ typedef struct {
     int64_t capacity;
 } rp_csr_out;
 
+/* Version of this header's signatures. Bumped whenever an exported function's arguments change
+ * (6: rp_dense_project_device gained `variant`; rp_project_stream_stats added); bindings compare
+ * rp_abi_version() with the value they were written against and refuse a mismatch, since a changed
+ * signature under the same symbol name cannot be detected otherwise. */
+#define RP_ABI_VERSION 6
+
 const char* rp_last_error(void);
 const char* rp_version(void);
+int rp_abi_version(void);
 /* sha256 prefix (16 hex digits) of the sources the library was built from (build.py); loaders
  * compare it with the sources on disk and refuse a stale binary. No reference counterpart. */
 const char* rp_build_id(void);
@@ -217,8 +224,13 @@ int rp_project_choice(const rp_projector* h, int64_t n_rows, int64_t nnz_a, cons
  * waits on its predecessors) and staging), or NULL to use the projector's own (then calls on one
  * projector must not run concurrently on different streams).
  * total_nnz: if non-NULL the call synchronizes the stream and stores the exact output nnz;
- * RP_ERR_CAPACITY is returned when it exceeds out->capacity (indptr is still complete).
- * If NULL the call is fully asynchronous (timing loops, graph capture). */
+ * RP_ERR_CAPACITY is returned when it exceeds out->capacity (indptr is still complete). In auto
+ * staging mode it also reads the sampling kernel's 4-byte verdict on the host and launches only the
+ * chosen branch (the staged kernels, or the direct main kernel for far-from-uniform columns).
+ * If NULL (with a caller workspace and a->nnz >= 0) the call never waits on the host (timing
+ * loops, graph capture): the verdict stays on the device and gates the staged kernels (same bits;
+ * the direct case then gathers inside the wave kernel, slower than the host-chosen branch on
+ * power-law columns). Under stream capture those three conditions are required (RP_ERR_INVALID). */
 int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int32_t order,
                       void* workspace, int64_t workspace_bytes, void* stream, int64_t* total_nnz);
 
@@ -251,6 +263,12 @@ int rp_project(rp_projector* h, const rp_csr_in* a_host, int32_t order, rp_alloc
  * checked on the device (RP_ERR_INVALID). Serialised per projector. */
 int rp_project_stream(rp_projector* h, const rp_csr_in* a_host, int32_t order, int64_t chunk_rows,
                       const rp_csr_out* c_host, int64_t* total_nnz);
+/* What the last rp_project_stream / rp_libsvm_project_stream call on this projector did: *chunks
+ * = chunks streamed; *recomputed = chunks whose output outgrew their device slot and were projected
+ * again alone after the pipeline drained (0 in the steady state: slot capacities follow the
+ * measured output per entry of the chunks already downloaded); *regrown = slot capacities raised
+ * from that measurement. Any out pointer may be NULL. No reference counterpart (diagnostics). */
+int rp_project_stream_stats(rp_projector* h, int64_t* chunks, int64_t* recomputed, int64_t* regrown);
 /* Page-locked host memory (hipHostMalloc) / its release. */
 int rp_host_alloc(int64_t bytes, void** out);
 int rp_host_free(void* p);

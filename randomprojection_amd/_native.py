@@ -15,16 +15,18 @@ RP_I32, RP_I64, RP_F32, RP_F64, RP_BF16 = 1, 2, 3, 4, 5
 RP_LAYOUT_AUTO, RP_LAYOUT_GENERIC, RP_LAYOUT_PACKED = 0, 1, 2
 RP_ORDER_SCIPY, RP_ORDER_SORTED = 0, 1
 RP_OPT_PIPELINE, RP_OPT_DEFER_POLLS, RP_OPT_DEFER_TICKS, RP_OPT_CHUNK_ROWS, RP_OPT_HOST_THREADS = 1, 2, 3, 4, 5
+# include/rp.h RP_ABI_VERSION these bindings are written against (signatures below)
+ABI_VERSION = 6
 
 # every symbol include/rp.h declares (tests/test_abi.py checks the .so exports them all)
 EXPORTS = (
-    "rp_last_error", "rp_version", "rp_build_id", "rp_device_count",
+    "rp_last_error", "rp_version", "rp_abi_version", "rp_build_id", "rp_device_count",
     "rp_projector_create", "rp_projector_info_get", "rp_projector_export",
     "rp_projector_create_from_device", "rp_projector_destroy", "rp_pack_r_host",
     "rp_project_workspace_bytes", "rp_project_workspace_bytes_for", "rp_project_plan", "rp_project_choice", "rp_projector_set_staging",
     "rp_projector_set_option", "rp_projector_get_option", "rp_project_device",
     "rp_project_host_begin", "rp_result_fetch", "rp_result_free", "rp_project",
-    "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_libsvm_project_stream", "rp_synth_libsvm_device", "rp_project_stream", "rp_host_alloc", "rp_host_free",
+    "rp_synth_rows_device", "rp_libsvm_parse_device", "rp_libsvm_project_stream", "rp_synth_libsvm_device", "rp_project_stream", "rp_project_stream_stats", "rp_host_alloc", "rp_host_free",
     "rp_dense_project_device",
 )
 
@@ -135,6 +137,7 @@ def load(path: str = None, verify: bool = None):
     sig = {
         "rp_last_error": (ctypes.c_char_p, []),
         "rp_version": (ctypes.c_char_p, []),
+        "rp_abi_version": (ctypes.c_int, []),
         "rp_build_id": (ctypes.c_char_p, []),
         "rp_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
         "rp_projector_create": (ctypes.c_int, [ctypes.c_int, i64, i64, vp, i32, vp, i32, vp, i32, i32, P(vp)]),
@@ -156,6 +159,7 @@ def load(path: str = None, verify: bool = None):
         "rp_result_free": (ctypes.c_int, [vp]),
         "rp_project": (ctypes.c_int, [vp, P(CsrIn), i32, ALLOC_FN, vp]),
         "rp_project_stream": (ctypes.c_int, [vp, P(CsrIn), i32, i64, P(CsrOut), P(i64)]),
+        "rp_project_stream_stats": (ctypes.c_int, [vp, P(i64), P(i64), P(i64)]),
         "rp_host_alloc": (ctypes.c_int, [i64, P(vp)]),
         "rp_host_free": (ctypes.c_int, [vp]),
         "rp_synth_rows_device": (ctypes.c_int, [ctypes.c_int, i64, i64, dbl, i32, i32, dbl, ctypes.c_uint64,
@@ -174,6 +178,9 @@ def load(path: str = None, verify: bool = None):
             raise NativeUnavailable(f"{path} does not export {name}: rebuild it")
         f.restype = res
         f.argtypes = args
+    if lib.rp_abi_version() != ABI_VERSION:
+        raise NativeUnavailable(f"{path} has ABI version {lib.rp_abi_version()}, these bindings are written "
+                                f"against {ABI_VERSION} (include/rp.h RP_ABI_VERSION): rebuild or update them")
     if verify:
         check_build_id(lib)
     _lib, _lib_path = lib, os.path.abspath(path)

@@ -8,6 +8,7 @@ stale binary under a fresh source hash."""
 from __future__ import annotations
 
 import fcntl
+import functools
 import hashlib
 import os
 import re
@@ -29,20 +30,34 @@ FLAGS = [
     "-ffp-contract=off", "-fno-fast-math", "-Wall",
 ]
 MARKER = b"rp-src-sha16:"
-HASHED = DEPS + ["randomprojection_amd/build.py"]  # files source_id covers (plus HIPCC and FLAGS)
+HASHED = DEPS + ["randomprojection_amd/build.py"]  # files source_id covers (plus the compiler and FLAGS)
+
+
+@functools.lru_cache(maxsize=None)
+def compiler_identity(hipcc: str = None) -> str:
+    """What ``hipcc --version`` reports (HIP and clang versions, target, install dir): the compiler
+    itself, not the path or environment variable that named it. A different compiler can change
+    the generated code (and with it bit-exactness), so it is part of the source id; the same
+    compiler reached through another path is not a reason to rebuild."""
+    try:
+        out = subprocess.run([hipcc or HIPCC, "--version"], capture_output=True, text=True, timeout=60)
+        return out.stdout.strip() if out.returncode == 0 else f"hipcc failed ({out.returncode})"
+    except (OSError, subprocess.TimeoutExpired) as e:
+        return f"hipcc unavailable ({type(e).__name__})"
 
 
 def source_id(root: str = ROOT) -> str:
     """sha256 prefix over (path, contents) of every source file of librp under ``root``, plus the
-    compiler path and flags and this build script (a changed flag such as -ffp-contract, which the
-    bit-exactness depends on, must rebuild and must make the loader refuse the old binary)."""
+    compiler's identity (``compiler_identity``), the flags and this build script (a changed flag
+    such as -ffp-contract, which the bit-exactness depends on, or another compiler version must
+    rebuild and must make the loader refuse the old binary)."""
     h = hashlib.sha256()
     for rel in HASHED:
         h.update(rel.encode() + b"\0")
         with open(os.path.join(root, rel), "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(("\0".join([HIPCC, *FLAGS])).encode())
+    h.update(("\0".join([compiler_identity(), *FLAGS])).encode())
     return h.hexdigest()[:16]
 
 

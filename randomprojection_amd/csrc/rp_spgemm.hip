@@ -2466,6 +2466,9 @@ struct rp_projector {
     int opt_defer_ticks = -1;   // -1 default
     int64_t opt_chunk_rows = 0; // 0 default
     int opt_host_threads = -1;  // -1 default
+    // the last stream call (rp_project_stream / rp_libsvm_project_stream): chunks, chunks recomputed
+    // after the pipeline (their output outgrew the device slot), slot regrowths in the pipeline
+    int64_t st_chunks = 0, st_redo = 0, st_regrow = 0;
     // generic
     DevBuf Bp, Bj, Bx32, Bx64;
     // internal workspace and host-path staging
@@ -2816,29 +2819,39 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
 // staging mode lpr_choose_kernel samples the call's feature ids first and the host reads its
 // verdict (4 bytes: the call's one wait, which lets only the chosen branch's kernels launch); a
 // caller may pass the choice instead (*choice >= 0: 1 staged, 0 direct; the stream pipelines reuse
-// their first chunk's), and gets back what was chosen.
+// their first chunk's), and gets back what was chosen. *choice == kChoiceOnDevice: the call must not
+// wait on the host (rp_project_device without total_nnz: timing loops, graph capture), so the
+// verdict stays on the device as the gate word and the staged branch is launched whatever it says:
+// with gate 0 the reserve, partition and gather kernels return at once and the wave kernel gathers
+// R's words directly (correct for any columns; on far-from-uniform columns slower than the direct
+// branch the host-read verdict launches).
+constexpr int kChoiceOnDevice = -2;
 template <typename T, typename IP, typename OP, typename OI>
 int launch_lpr(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, int order,
                Workspace* ws, const Plan& pl, hipStream_t st, int* choice) {
     const int64_t n = a->n_rows, step = std::max<int64_t>(pl.lpr_chunk, 1);
     uint32_t* gate = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(ws) + pl.carry + 16);
-    bool staged = pl.staged;
-    if (pl.gated && n > 0) {  // staged or direct for this call: sampled on the device, read here
+    bool staged = pl.staged, on_device = false;
+    if (pl.gated && n > 0) {  // staged or direct for this call: sampled on the device
         if (choice && *choice >= 0) {
             staged = *choice != 0;
         } else {
             hipLaunchKernelGGL((lpr_choose_kernel<IP>), dim3(1), dim3(1024), 0, st, (const IP*)a->indptr, a->indices, n,
                                gate);
             HIP_TRY(hipGetLastError());
-            uint32_t g = 0;
-            HIP_TRY(hipMemcpyAsync(&g, gate, 4, hipMemcpyDeviceToHost, st));
-            HIP_TRY(poll_stream(st));
-            staged = g != 0;
+            if (choice && *choice == kChoiceOnDevice) {
+                on_device = true;  // the gate word carries the verdict to the staged kernels
+            } else {
+                uint32_t g = 0;
+                HIP_TRY(hipMemcpyAsync(&g, gate, 4, hipMemcpyDeviceToHost, st));
+                HIP_TRY(poll_stream(st));
+                staged = g != 0;
+            }
         }
     }
-    if (choice) *choice = staged ? 1 : 0;
+    if (choice && !on_device) *choice = staged ? 1 : 0;
     // the gate: staged until a segment overflows; 0 records a direct call (rp_project_choice)
-    if (pl.staged) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)gate, staged ? 1u : 0u, 1, st));
+    if (pl.staged && !on_device) HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)gate, staged ? 1u : 0u, 1, st));
     int64_t k = 0;
     for (int64_t r0 = 0; r0 < n; r0 += step, ++k) {
         rp_csr_in sa = *a;
@@ -2947,16 +2960,13 @@ int project_device_impl(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c
     }
     HIP_TRY(hipMemsetAsync(ws, 0, plan.zero, st));  // header + look-back states only
     if (n_tiles == 0) {
-        // empty A: indptr = [0]
-        if (c->indptr_type == RP_I64) {
-            int64_t z = 0;
-            HIP_TRY(hipMemcpyAsync(c->indptr, &z, 8, hipMemcpyHostToDevice, st));
-        } else {
-            int32_t z = 0;
-            HIP_TRY(hipMemcpyAsync(c->indptr, &z, 4, hipMemcpyHostToDevice, st));
+        // empty A: indptr = [0] (a memset: no host source, so nothing to wait for unless asked)
+        HIP_TRY(hipMemsetAsync(c->indptr, 0, (size_t)dtype_size(c->indptr_type), st));
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&ws->staged_used, 0, 1, st));
+        if (total_nnz) {
+            HIP_TRY(hipStreamSynchronize(st));
+            *total_nnz = 0;
         }
-        HIP_TRY(hipStreamSynchronize(st));
-        if (total_nnz) *total_nnz = 0;
         return RP_OK;
     }
     if (h->layout == RP_LAYOUT_PACKED) {
@@ -3103,6 +3113,8 @@ extern "C" {
 
 const char* rp_last_error(void) { return g_err.c_str(); }
 const char* rp_version(void) { return "rp-mi355x 0.1 (gfx950)"; }
+
+int rp_abi_version(void) { return RP_ABI_VERSION; }
 
 // The sha256 prefix of every source this library was compiled from (build.py passes it as
 // RP_SRC_SHA16 and also finds it in the binary through the marker), so a benched or tested number
@@ -3427,6 +3439,17 @@ int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, 
                       void* workspace, int64_t workspace_bytes, void* stream, int64_t* total_nnz) {
     if (!h) return fail(RP_ERR_INVALID, "NULL projector");
     if (order != RP_ORDER_SCIPY && order != RP_ORDER_SORTED) return fail(RP_ERR_INVALID, "bad order");
+    HIP_TRY(hipSetDevice(h->device));
+    // under stream capture nothing may wait on the host: the caller's workspace, a known nnz(A) and
+    // no total_nnz are then required (each of the others makes the call synchronise)
+    hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing((hipStream_t)stream, &cap_status) != hipSuccess) {
+        (void)hipGetLastError();  // the legacy stream cannot capture; clear the sticky error
+        cap_status = hipStreamCaptureStatusNone;
+    }
+    if (cap_status != hipStreamCaptureStatusNone && (total_nnz || !workspace || !a || a->nnz < 0))
+        return fail(RP_ERR_INVALID, "under stream capture rp_project_device needs a caller workspace, a->nnz >= 0 "
+                                    "and total_nnz == NULL (each of these would wait on the host)");
     // nnz(A) for tile sizing: given, or read from the two ends of indptr (tiny D2H)
     int64_t nnz_a = a ? a->nnz : -1;
     if (a && nnz_a < 0 && a->n_rows > 0 && a->indptr) {
@@ -3453,8 +3476,10 @@ int rp_project_device(rp_projector* h, const rp_csr_in* a, const rp_csr_out* c, 
         if (rc == RP_OK) HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
         return rc;
     }
+    // without total_nnz the call is fully asynchronous: the staging verdict stays on the device
+    int choice = total_nnz ? -1 : kChoiceOnDevice;
     return project_device_impl(h, a, c, order, workspace, workspace_bytes, (hipStream_t)stream,
-                               total_nnz, nnz_a);
+                               total_nnz, nnz_a, &choice);
 }
 
 int rp_project_host_begin(rp_projector* h, const rp_csr_in* a, int32_t order, rp_result** out,
@@ -3748,6 +3773,18 @@ struct StreamChunk {
     int64_t r0, rows, e0, nnz;
 };
 
+// Device output capacity of a stream slot for a chunk of `nnz` entries. The first chunks have only
+// R's mean row length to go by (ppe = R.nnz / m: the expected products per entry for uniform
+// columns), so they get 25% headroom on it; once chunks have come back, the largest measured output
+// per entry (`seen`, the exact nnz of downloaded chunks / their entries) + 10% governs. Power-law
+// columns shift the mean R row length under an entry (Zipf(1.1) on KDD2012's R: 0.576 kept outputs
+// per entry vs 0.554 uniform), which a slot sized at 1.02x the uniform expectation did not hold:
+// every chunk was recomputed alone after the pipeline (76 M rows/s instead of ~540 M).
+int64_t stream_slot_cap(double ppe, double seen, int64_t nnz) {
+    const double ex = std::max(1.25 * ppe, 1.10 * seen) * (double)nnz;
+    return (int64_t)(ex + 8.0 * std::sqrt(ex + 1.0)) + 4096;
+}
+
 struct StreamSync {
     std::mutex mu;
     std::condition_variable cv;
@@ -3942,11 +3979,14 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
         if (total_nnz) *total_nnz = 0;
         return RP_OK;
     }
-    // device output capacity per slot: the expected products of the largest chunk + 6 sigma; a
-    // chunk beyond it is recomputed alone once the pipeline has drained
+    // device output capacity per slot (stream_slot_cap): from R's mean row length for the first
+    // chunks, then from the measured output per entry of the chunks already downloaded (a slot
+    // grows before it takes a chunk that would not fit); a chunk beyond its slot anyway is
+    // recomputed alone once the pipeline has drained (counted: rp_project_stream_stats)
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
-    const double expect = ppe * (double)max_nnz;
-    const int64_t cap = (int64_t)(1.02 * expect + 8.0 * std::sqrt(expect + 1.0)) + 4096;
+    const int64_t cap = stream_slot_cap(ppe, 0.0, max_nnz);
+    h->st_chunks = (int64_t)chunks.size();
+    h->st_redo = h->st_regrow = 0;
     StreamSlot slots[kStreamSlots];
     const int ns = (int)std::min<size_t>(kStreamSlots, chunks.size());
     int rc;
@@ -4003,8 +4043,22 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
             sy.bump(sy.downloaded);
         }
     });
+    double seen = 0.0;  // largest output per entry of the chunks downloaded so far
+    int64_t folded = 0;
     for (int64_t k = 0; k < K && sy.err == RP_OK; ++k) {
         if (!sy.wait([&] { return sy.uploaded > k && sy.downloaded >= k - ns + 1; })) break;
+        for (; folded <= k - ns; ++folded)  // downloaded (the wait above): knnz is final
+            if (chunks[(size_t)folded].nnz > 0)
+                seen = std::max(seen, (double)knnz[(size_t)folded] / (double)chunks[(size_t)folded].nnz);
+        StreamSlot& sk = slots[k % ns];
+        const int64_t want = stream_slot_cap(ppe, seen, chunks[(size_t)k].nnz);
+        if (want > sk.cap) {  // the slot's previous chunk has been downloaded: its output may move
+            if ((rc = stream_alloc_slot(h, sk, max_rows, max_nnz, want, ips, vs, c->indptr_type, c->indices_type))) {
+                sy.set_error(rc);
+                break;
+            }
+            ++h->st_regrow;
+        }
         if ((rc = stream_compute(h, a, chunks[(size_t)k], slots[k % ns], order, a->indptr_type, a->data_type,
                                  c->indptr_type, c->indices_type, (unsigned long long*)totbuf.p, k == K - 1,
                                  st_comp, &choice))) {
@@ -4026,6 +4080,7 @@ int rp_project_stream(rp_projector* h, const rp_csr_in* a, int32_t order, int64_
     for (int64_t k = 0; k < K; ++k) total += knnz[(size_t)k];
     for (int64_t k = 0; k < K && rc == RP_OK; base += knnz[(size_t)k], ++k) {
         if (!redo[(size_t)k]) continue;
+        ++h->st_redo;
         StreamSlot& s = slots[0];
         const StreamChunk& ck = chunks[(size_t)k];
         if ((rc = stream_alloc_slot(h, s, max_rows, max_nnz, knnz[(size_t)k], ips, vs, c->indptr_type,
@@ -4141,10 +4196,10 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
         return fail(RP_ERR_HIP, "stream setup failed");
     }
     const double ppe = h->m > 0 ? (double)h->nnz / (double)h->m : 0.0;
-    auto out_cap = [&](int64_t nnz) {
-        const double ex = ppe * (double)nnz;
-        return (int64_t)(1.05 * ex + 8.0 * std::sqrt(ex + 1.0)) + 4096;
-    };
+    double seen = 0.0;  // largest output per entry of the chunks downloaded so far (stream_slot_cap)
+    auto out_cap = [&](int64_t nnz) { return stream_slot_cap(ppe, seen, nnz); };
+    h->st_chunks = (int64_t)chunks.size();
+    h->st_redo = h->st_regrow = 0;
     const int dev = h->device;
     const int64_t K = (int64_t)chunks.size();
     StreamSync sy;
@@ -4166,6 +4221,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
                              nullptr, 0, 0, st_comp, &rows, &nnz, &el);
         if (r) return r;
         const int64_t cap = cap_out >= 0 ? cap_out : out_cap(nnz);
+        if (cap_out < 0 && 1.10 * seen > 1.25 * ppe) ++h->st_regrow;  // sized from measured output
         if ((r = t.labels.grow(8 * (size_t)std::max<int64_t>(rows, 1), dev)) ||
             (r = stream_alloc_slot(h, t.s, rows, nnz, cap, 8, 4, c->indptr_type, c->indices_type)))
             return r;
@@ -4207,9 +4263,12 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
             sy.bump(sy.downloaded);
         }
     });
-    int64_t rows_total = 0;
+    int64_t rows_total = 0, folded = 0;
     for (int64_t k = 0; k < K && sy.err == RP_OK; ++k) {
         if (!sy.wait([&] { return sy.uploaded > k && sy.downloaded >= k - ns + 1; })) break;
+        for (; folded <= k - ns; ++folded)  // downloaded (the wait above): knnz is final
+            if (cks[(size_t)folded].nnz > 0)
+                seen = std::max(seen, (double)knnz[(size_t)folded] / (double)cks[(size_t)folded].nnz);
         TextSlot& t = slots[k % ns];
         if ((rc = parse(k, t, -1))) {
             sy.set_error(rc);
@@ -4244,6 +4303,7 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
     rc = RP_OK;
     for (int64_t k = 0; k < K && rc == RP_OK; base += knnz[(size_t)k], ++k) {
         if (!redo[(size_t)k]) continue;
+        ++h->st_redo;
         TextSlot& t = slots[0];
         const int64_t r0 = cks[(size_t)k].r0;
         if ((rc = upload(k, t)) || (rc = parse(k, t, knnz[(size_t)k]))) break;
@@ -4270,6 +4330,15 @@ int rp_libsvm_project_stream(rp_projector* h, const char* text, int64_t n_bytes,
         return fail(RP_ERR_CAPACITY, "output capacity %lld < nnz %lld", (long long)c->capacity, (long long)total);
     if (c->indptr_type == RP_I32 && total > INT32_MAX)
         return fail(RP_ERR_CAPACITY, "nnz %lld needs an int64 output indptr", (long long)total);
+    return RP_OK;
+}
+
+int rp_project_stream_stats(rp_projector* h, int64_t* chunks, int64_t* recomputed, int64_t* regrown) {
+    if (!h) return fail(RP_ERR_INVALID, "NULL projector");
+    std::lock_guard<std::mutex> lock(h->mu);  // the stream calls hold it while they run
+    if (chunks) *chunks = h->st_chunks;
+    if (recomputed) *recomputed = h->st_redo;
+    if (regrown) *regrown = h->st_regrow;
     return RP_OK;
 }
 

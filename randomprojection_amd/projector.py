@@ -253,6 +253,15 @@ class Projector:
                 Cp, Cj = Cp.astype(want), Cj[:k].astype(want)
         return Cp, Cj[:k], Cx[:k]
 
+    def stream_stats(self) -> dict:
+        """What the last stream call (``project_stream`` / the libsvm stream) did
+        (rp_project_stream_stats): chunks streamed, chunks recomputed after the pipeline because
+        their output outgrew the device slot (0 in the steady state), slot capacities raised from
+        the measured output per entry."""
+        ch, rd, rg = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        nat.check(self._lib.rp_project_stream_stats(self._h, ctypes.byref(ch), ctypes.byref(rd), ctypes.byref(rg)))
+        return {"chunks": int(ch.value), "recomputed": int(rd.value), "regrown": int(rg.value)}
+
     def matmul(self, A, order: str = "scipy"):
         """``A @ R`` for sparse A, returning what scipy returns (container of A's class)."""
         if not sp.issparse(A):
@@ -272,7 +281,10 @@ class Projector:
         uint8 tensor (or a ``(pointer, bytes)`` pair) of ``workspace_bytes(n, nnz)``, or None.
 
         Returns the exact output nnz when ``sync`` (raises ``RPError`` with code RP_ERR_CAPACITY
-        if ``Cj``/``Cx`` are too small), else None (fully asynchronous launch on ``stream``)."""
+        if ``Cj``/``Cx`` are too small; in auto staging mode the host reads the device's staging
+        verdict and launches only the chosen branch), else None: the launch never waits on the host
+        (the verdict gates the staged kernels on the device), so it can be captured in a graph when
+        ``workspace`` is given and ``nnz_a >= 0``."""
         def p_(t):
             return int(t.data_ptr()) if hasattr(t, "data_ptr") else int(t)
 

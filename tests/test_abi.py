@@ -99,3 +99,23 @@ def test_committed_traffic_matches_sources():
         tj = json.load(f)
     assert tj["src_sha16"] == build.source_id()
     assert tj["hbm_bytes_per_launch"] > 0
+
+
+def test_source_id_follows_the_compiler_not_its_path(monkeypatch):
+    """The id hashes what ``hipcc --version`` reports: the same compiler reached through another
+    path keeps the id (no spurious rebuild), another compiler identity changes it."""
+    from randomprojection_amd import build
+
+    sid = build.source_id()
+    real = os.path.realpath(build.HIPCC)
+    assert build.compiler_identity(real) == build.compiler_identity()
+    monkeypatch.setattr(build, "compiler_identity", lambda hipcc=None: "AMD clang version 0.0 (other)")
+    assert build.source_id() != sid
+
+
+def test_abi_version_matches_bindings():
+    """rp_abi_version() equals include/rp.h's RP_ABI_VERSION and the bindings' ABI_VERSION (a changed
+    signature under an old symbol name is refused at load time instead of passing garbage)."""
+    src = open(os.path.join(ROOT, "include", "rp.h")).read()
+    want = int(re.search(r"#define RP_ABI_VERSION (\d+)", src).group(1))
+    assert nat.load().rp_abi_version() == want == nat.ABI_VERSION

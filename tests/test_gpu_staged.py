@@ -418,3 +418,56 @@ def test_auto_staging_choice_on_device(dist):
     for mode, (cp, cj, cx) in outs.items():
         assert np.array_equal(cp, want[0]) and np.array_equal(cj, want[1]), mode
         assert np.array_equal(cx.view(np.uint32), want[2].view(np.uint32)), mode
+
+
+@pytest.mark.parametrize("dist", ["uniform", "powerlaw"])
+def test_auto_staging_async_and_graph_capture(dist):
+    """Auto mode without total_nnz (``sync=False``) never waits on the host: the sampled verdict stays
+    on the device and gates the staged kernels (power-law columns: the reserve/partition/gather
+    kernels return at once and the wave kernel gathers directly). The same call captured in a HIP
+    graph and replayed gives the same bits; the sync form's output is the reference (the oracle
+    checks it in test_auto_staging_choice_on_device). Under capture, a call that would wait on the
+    host (total_nnz asked) is refused before anything is enqueued."""
+    import torch
+    from randomprojection_amd import _native as nat
+    from randomprojection_amd import synth
+
+    m, p, n = 10_000_000, 256, 420_000
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    Ap, Aj, Ax = synth.kdd_rows_device(n, m, seed=34, dist=dist)
+    nnz_a = int(Aj.numel())
+    P = Projector(R)
+    assert P.plan(n, nnz_a)["staged"] == "auto"
+    ws = torch.empty(P.workspace_bytes(n, nnz_a), dtype=torch.uint8, device="cuda")
+    cap = int(3 * nnz_a * P.nnz / P.m) + 65536
+
+    def outs():
+        return (torch.empty(n + 1, dtype=torch.int32, device="cuda"), torch.empty(cap, dtype=torch.int32, device="cuda"),
+                torch.empty(cap, dtype=torch.float32, device="cuda"))
+
+    Cp, Cj, Cx = outs()
+    k = P.project_device(Ap, Aj, Ax, Cp, Cj, Cx, workspace=ws, nnz_a=nnz_a)
+    ref = (Cp.clone(), Cj[:k].clone(), Cx[:k].clone())
+    side = torch.cuda.Stream()
+    Dp, Dj, Dx = outs()
+    with torch.cuda.stream(side):
+        assert P.project_device(Ap, Aj, Ax, Dp, Dj, Dx, workspace=ws, nnz_a=nnz_a, stream=side.cuda_stream,
+                                sync=False) is None
+    side.synchronize()
+    assert P.choice(n, nnz_a, ws) == (dist == "uniform")
+    assert torch.equal(Dp, ref[0]) and torch.equal(Dj[:k], ref[1]) and torch.equal(Dx[:k].view(torch.int32),
+                                                                                 ref[2].view(torch.int32))
+    Gp, Gj, Gx = outs()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        P.project_device(Ap, Aj, Ax, Gp, Gj, Gx, workspace=ws, nnz_a=nnz_a, stream=side.cuda_stream, sync=False)
+        with pytest.raises(nat.RPError, match="stream capture"):
+            P.project_device(Ap, Aj, Ax, Gp, Gj, Gx, workspace=ws, nnz_a=nnz_a, stream=side.cuda_stream)
+    for _ in range(2):
+        Gj.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(Gp, ref[0]) and torch.equal(Gj[:k], ref[1]) and torch.equal(Gx[:k].view(torch.int32),
+                                                                                     ref[2].view(torch.int32))
+    del g
+    P.close()

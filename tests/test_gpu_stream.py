@@ -76,6 +76,31 @@ def test_stream_chunk_beyond_slot_capacity_recomputed():
     Cp, Cj, Cx, _, _ = smmp.matmat(A, R)
     ip, ix, dx = P.project_stream(A.indptr, A.indices, A.data, chunk_rows=100_000)
     assert np.array_equal(ip, Cp) and np.array_equal(ix, Cj) and same_bits(dx, Cx)
+    # chunks 4 and 5 are the heavy ones; when they launch only uniform chunks have come back
+    assert P.stream_stats() == {"chunks": 6, "recomputed": 2, "regrown": 0}
+
+
+def test_stream_slots_follow_measured_output():
+    """Every row hits R's densest rows (~3x the outputs per entry R's mean row length predicts):
+    the first kStreamSlots = 3 chunks are launched before any has come back and are recomputed;
+    from then on each slot grows to the measured output per entry before it takes its next chunk,
+    so no later chunk is recomputed. Bit-exact either way (scipy csr_matmat, the oracle)."""
+    m, p = 300_000, 2048
+    R = sm.projection_operand(sm.sparse_random_matrix(p, m, random_state=123))
+    P = Projector(R)
+    heavy = np.argsort(np.diff(R.indptr))[-64:].astype(np.int32)
+    rng = np.random.default_rng(7)
+    n = 500_000
+    k = 1 + rng.poisson(6, size=n)
+    cols = [np.unique(rng.choice(heavy, size=int(x))) for x in k]
+    indptr = np.concatenate([[0], np.cumsum([c.size for c in cols])]).astype(np.int64)
+    A = sp.csr_matrix((rng.standard_normal(indptr[-1]).astype(np.float32), np.concatenate(cols), indptr),
+                      shape=(n, m))
+    Cp, Cj, Cx, _, _ = smmp.matmat(A, R)
+    ip, ix, dx = P.project_stream(A.indptr, A.indices, A.data, chunk_rows=50_000)
+    assert np.array_equal(ip, Cp) and np.array_equal(ix, Cj) and same_bits(dx, Cx)
+    st = P.stream_stats()
+    assert st["chunks"] == 10 and st["recomputed"] == 3 and 3 <= st["regrown"] <= 7, st
 
 
 def test_stream_errors(setup):
