@@ -15,6 +15,7 @@ RP_I32, RP_I64, RP_F32, RP_F64, RP_BF16 = 1, 2, 3, 4, 5
 RP_LAYOUT_AUTO, RP_LAYOUT_GENERIC, RP_LAYOUT_PACKED = 0, 1, 2
 RP_ORDER_SCIPY, RP_ORDER_SORTED = 0, 1
 RP_OPT_PIPELINE, RP_OPT_DEFER_POLLS, RP_OPT_DEFER_TICKS, RP_OPT_CHUNK_ROWS, RP_OPT_HOST_THREADS = 1, 2, 3, 4, 5
+RP_OPT_FUSED_COPY = 8
 # include/rp.h RP_ABI_VERSION these bindings are written against (signatures below)
 ABI_VERSION = 6
 
@@ -89,7 +90,11 @@ def check_build_id(lib, root: str = None) -> str:
     from . import build as _build
 
     have = lib.rp_build_id().decode()
-    want = _build.source_id(root or _build.ROOT)
+    # the compiler identity recorded in the binary at build time (no compiler run here)
+    cc = _build.library_cc(getattr(lib, "_name", None) or LIB_PATH)
+    if cc is None:
+        raise StaleLibrary("librp carries no compiler identity: rebuild it (python -m randomprojection_amd.build)")
+    want = _build.source_id(root or _build.ROOT, cc=cc)
     if have != want:
         raise StaleLibrary(f"librp was built from sources {have}, the sources on disk are {want}: rebuild it "
                            "(python -m randomprojection_amd.build); numbers from a stale binary are refused")

@@ -30,15 +30,15 @@ FLAGS = [
     "-ffp-contract=off", "-fno-fast-math", "-Wall",
 ]
 MARKER = b"rp-src-sha16:"
+CC_MARKER = b"rp-cc-sha16:"
 HASHED = DEPS + ["randomprojection_amd/build.py"]  # files source_id covers (plus the compiler and FLAGS)
 
 
 @functools.lru_cache(maxsize=None)
 def compiler_identity(hipcc: str = None) -> str:
     """What ``hipcc --version`` reports (HIP and clang versions, target, install dir): the compiler
-    itself, not the path or environment variable that named it. A different compiler can change
-    the generated code (and with it bit-exactness), so it is part of the source id; the same
-    compiler reached through another path is not a reason to rebuild."""
+    itself, not the path or environment variable that named it. Only builds run it (a loader must
+    not start a child process: under a GPU profiler the process has initialised the GPU already)."""
     try:
         out = subprocess.run([hipcc or HIPCC, "--version"], capture_output=True, text=True, timeout=60)
         return out.stdout.strip() if out.returncode == 0 else f"hipcc failed ({out.returncode})"
@@ -46,30 +46,46 @@ def compiler_identity(hipcc: str = None) -> str:
         return f"hipcc unavailable ({type(e).__name__})"
 
 
-def source_id(root: str = ROOT) -> str:
+def compiler_hash(hipcc: str = None) -> str:
+    """16-hex-digit sha256 prefix of ``compiler_identity``; builds embed it in the library
+    (``RP_CC_SHA16``) so that a loader can recompute the source id without running the compiler."""
+    return hashlib.sha256(compiler_identity(hipcc).encode()).hexdigest()[:16]
+
+
+def source_id(root: str = ROOT, cc: str = None) -> str:
     """sha256 prefix over (path, contents) of every source file of librp under ``root``, plus the
-    compiler's identity (``compiler_identity``), the flags and this build script (a changed flag
-    such as -ffp-contract, which the bit-exactness depends on, or another compiler version must
-    rebuild and must make the loader refuse the old binary)."""
+    compiler's identity hash ``cc`` (default: the compiler HIPCC names now, ``compiler_hash``), the
+    flags and this build script: a changed flag such as -ffp-contract, which the bit-exactness
+    depends on, or another compiler version must rebuild, and the loader (which takes ``cc`` from
+    the library it loads) must refuse a binary built from other sources."""
     h = hashlib.sha256()
     for rel in HASHED:
         h.update(rel.encode() + b"\0")
         with open(os.path.join(root, rel), "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(("\0".join([compiler_identity(), *FLAGS])).encode())
+    h.update(("\0".join([cc or compiler_hash(), *FLAGS])).encode())
     return h.hexdigest()[:16]
 
 
-def library_id(path: str = OUT) -> str | None:
-    """The source id a built library carries (read from the binary, without loading it)."""
+def _marker(path: str, marker: bytes) -> str | None:
     try:
         with open(path, "rb") as f:
             blob = f.read()
     except OSError:
         return None
-    m = re.search(re.escape(MARKER) + rb"([0-9a-f]{16}|unknown)\0", blob)
+    m = re.search(re.escape(marker) + rb"([0-9a-f]{16}|unknown)\0", blob)
     return m.group(1).decode() if m else None
+
+
+def library_cc(path: str = None) -> str | None:
+    """The compiler identity hash a built library carries (read from the binary, without loading it)."""
+    return _marker(path or OUT, CC_MARKER)
+
+
+def library_id(path: str = OUT) -> str | None:
+    """The source id a built library carries (read from the binary, without loading it)."""
+    return _marker(path, MARKER)
 
 
 def needs_build(out: str = OUT) -> bool:
@@ -89,8 +105,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 def _compile_and_link(out: str, verbose: bool) -> None:
-    sid = source_id()
-    extra = [f'-DRP_SRC_SHA16="{sid}"']
+    cc = compiler_hash()
+    sid = source_id(cc=cc)
+    extra = [f'-DRP_SRC_SHA16="{sid}"', f'-DRP_CC_SHA16="{cc}"']
     odir = os.path.join(HERE, "build", "rel")
     os.makedirs(odir, exist_ok=True)
     objs, procs = [], []

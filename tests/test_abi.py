@@ -109,6 +109,11 @@ def test_source_id_follows_the_compiler_not_its_path(monkeypatch):
     sid = build.source_id()
     real = os.path.realpath(build.HIPCC)
     assert build.compiler_identity(real) == build.compiler_identity()
+    # the library records the identity it was built with: the loader recomputes the id from it
+    # without running the compiler (a child process of a GPU-initialised process is refused on
+    # the GPU box)
+    assert build.library_cc(nat.LIB_PATH) == build.compiler_hash()
+    assert build.source_id(cc=build.library_cc(nat.LIB_PATH)) == sid
     monkeypatch.setattr(build, "compiler_identity", lambda hipcc=None: "AMD clang version 0.0 (other)")
     assert build.source_id() != sid
 
