@@ -187,9 +187,6 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
  *                        whole 256-row tiles
  *   RP_OPT_HOST_THREADS  helper threads of the host result download: -1 default (min(4, cores));
  *                        0 or 1 plain copies
- *   RP_OPT_FUSED_COPY    staged row-lane pipeline: -1 default (on), 0 off, 1 on — copy workers
- *                        inside the wave kernel move finished units to C while later units are
- *                        still computed (otherwise a copy kernel runs after it)
  * (Options 6 and 7 — the persistent row-lane kernel and the filtered tile pipeline, both measured
  * slower than the defaults — were removed in round 5 and are rejected as unknown.) */
 typedef enum {
@@ -197,8 +194,7 @@ typedef enum {
     RP_OPT_DEFER_POLLS = 2,
     RP_OPT_DEFER_TICKS = 3,
     RP_OPT_CHUNK_ROWS = 4,
-    RP_OPT_HOST_THREADS = 5,
-    RP_OPT_FUSED_COPY = 8
+    RP_OPT_HOST_THREADS = 5
 } rp_option;
 int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value);
 int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* value);

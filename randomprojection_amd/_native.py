@@ -15,7 +15,6 @@ RP_I32, RP_I64, RP_F32, RP_F64, RP_BF16 = 1, 2, 3, 4, 5
 RP_LAYOUT_AUTO, RP_LAYOUT_GENERIC, RP_LAYOUT_PACKED = 0, 1, 2
 RP_ORDER_SCIPY, RP_ORDER_SORTED = 0, 1
 RP_OPT_PIPELINE, RP_OPT_DEFER_POLLS, RP_OPT_DEFER_TICKS, RP_OPT_CHUNK_ROWS, RP_OPT_HOST_THREADS = 1, 2, 3, 4, 5
-RP_OPT_FUSED_COPY = 8
 # include/rp.h RP_ABI_VERSION these bindings are written against (signatures below)
 ABI_VERSION = 6
 

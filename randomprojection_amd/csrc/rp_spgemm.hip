@@ -1241,51 +1241,13 @@ struct LprSpace {
     uint32_t* hlist;      // heavy tiles, count in ws->n_deferred
     uint32_t* tflag;      // n_tiles: 1 = heavy (lpr_heavy_write places the tile)
     uint32_t* rowmeta;    // n_tiles x 256: the row's slot range, kst | kept << 16 (lpr_store_slot)
-    uint16_t* cols;       // 4 x n_tiles x cstride (a wave's columns start on a 128-B line)
-    unsigned char* vals;  // 4 x n_tiles x slot x sizeof(T) (slot is a multiple of 32: lines too)
+    uint16_t* cols;       // 4 x n_tiles x slot
+    unsigned char* vals;  // 4 x n_tiles x slot x sizeof(T)
     unsigned long long* scan_state;  // one per 4096-wave scan block
-    uint32_t slot;        // kept-entry capacity of one wave
-    uint32_t cstride;     // column entries per wave in `cols`: slot rounded up to 64 (128 B)
+    uint32_t slot;        // kept-entry capacity of one wave (a multiple of 32)
 };
-__host__ __device__ inline uint32_t lpr_cstride(uint32_t slot) { return (slot + 63) & ~63u; }
 
-// Copy workers fused into the staged wave kernel (RP_OPT_FUSED_COPY): the first n_workers
-// workgroups of its grid take super-tiles (8 units) in row order from `ticket`, wait until their
-// 8 units have signalled (ag), find the super-tile's output offset by a decoupled look-back over
-// the super-tile states `st` among themselves, and move the units' slots to C while later units are
-// still being computed (the copy's HBM traffic under the VALU-bound wave kernel instead of after
-// it). A unit signals after its slot, row metadata and count are stored write-through (sc1) and
-// drained (vmcnt(0)): one agent-scope atomic add of (1 << 48 | its kept entries) to ag[super-tile],
-// (1 << 47) instead when it goes heavy. A super-tile with a heavy unit publishes the prefix
-// kXVal: no later look-back can resolve a prefix through it, so everything from there on is
-// left to the scan + lpr_copy_kernel (+ lpr_heavy_write) as without fusion; `placed` marks what the
-// workers wrote (lpr_copy_kernel skips it). Producers never wait, so the workers (256 one-wave
-// workgroups dispatched first: a few percent of the wave slots) cannot deadlock the grid.
-struct LprFuse {
-    unsigned long long* ag;     // per super-tile: units done << 48 | heavy << 47 | kept entries
-    unsigned long long* st;     // per super-tile look-back states (kFlagA / kFlagP granules)
-    uint32_t* placed;           // per super-tile: 1 = placed by the workers
-    unsigned int* ticket;       // next super-tile for a worker
-    const unsigned long long* base_in;  // the chunk's carry: output entries of the earlier chunks
-    void* Cp;
-    void* Cj;
-    void* Cx;
-    unsigned long long capacity;
-    unsigned n_workers;         // 0: not fused
-    int op64, oi64;             // output indptr / indices int64
-};
-constexpr unsigned kFuseWorkers = 256;
-constexpr uint64_t kXVal = 1ull << 52;  // a super-tile prefix that cannot be resolved (heavy unit)
-constexpr int kAuxNT = 2, kAuxSC1 = 16;  // buffer instruction cache policy: nt / sc1 (gfx950)
-// buffer stores with a (uniform) runtime choice of the two policies (the builtin takes a constant)
-__device__ __forceinline__ void st_b32(uint32_t v, __amdgpu_buffer_rsrc_t r, uint32_t off, int aux) {
-    if (aux == kAuxSC1) __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, kAuxSC1);
-    else __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, kAuxNT);
-}
-__device__ __forceinline__ void st_b128(v4u v, __amdgpu_buffer_rsrc_t r, uint32_t off, int aux) {
-    if (aux == kAuxSC1) __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxSC1);
-    else __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxNT);
-}
+constexpr int kAuxNT = 2;  // buffer instruction cache policy: nt (gfx950)
 
 __device__ __forceinline__ uint32_t lpr_h2(uint32_t col) { return (col * 0x9E3779B1u) >> 26; }
 
@@ -1329,7 +1291,7 @@ template <typename T>
 __device__ __forceinline__ uint32_t lpr_store_slot(uint16_t* cb, T* vb, uint32_t kst, uint32_t kept,
                                                    bool valid, int lane, uint32_t extent, int order,
                                                    uint32_t* __restrict__ rowmeta, uint32_t* __restrict__ cnt,
-                                                   uint16_t* __restrict__ oc, T* __restrict__ ov, int aux = kAuxNT) {
+                                                   uint16_t* __restrict__ oc, T* __restrict__ ov) {
     const uint32_t c = valid ? kept : 0u;
     const uint32_t incl = wave_scan_dpp(c);
     const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
@@ -1347,19 +1309,19 @@ __device__ __forceinline__ uint32_t lpr_store_slot(uint16_t* cb, T* vb, uint32_t
             }
         __builtin_amdgcn_wave_barrier();
     }
-    // 16 bytes per lane and store (8 columns, 16 / sizeof(T) values), `aux` the cache policy: nt,
-    // or sc1 (write-through) for a fused copy worker's hand-off. The slot's regions start on 128-B
-    // lines and hold slot (a multiple of 32) entries, so the rounded-up tail stays inside them.
-    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)rowmeta, (short)0, 256, 0x00020000);
-    st_b32(kst | (c << 16), rm, valid ? 4u * lane : 0x80000000u, aux);
+    // 16 bytes per lane and store (8 columns, 16 / sizeof(T) values), non-temporal. A wave's slot
+    // regions start 16-B aligned and hold slot (a multiple of 32) entries: the rounded-up tail
+    // stays inside them.
+    if (valid) rowmeta[lane] = kst | (c << 16);
     if (lane == 0) *cnt = tot;
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)oc, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)ov, (short)0, 0x7fffffff, 0x00020000);
     for (uint32_t o = 8 * lane; o < extent; o += 512)
-        st_b128(*reinterpret_cast<const v4u*>(cb + o), rc, 2 * o, aux);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u*>(cb + o), rc, 2 * o, 0, kAuxNT);
     constexpr uint32_t kPer = 16 / sizeof(T);
     for (uint32_t o = kPer * lane; o < extent; o += 64 * kPer)
-        st_b128(*reinterpret_cast<const v4u*>(vb + o), rv, (uint32_t)sizeof(T) * o, aux);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u*>(vb + o), rv, (uint32_t)sizeof(T) * o, 0,
+                                               kAuxNT);
     return tot;
 }
 
@@ -1742,127 +1704,10 @@ lpr_main_flat_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap
     __builtin_amdgcn_wave_barrier();
     const size_t wt = (size_t)tile * 4 + w;
     lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, order, sp.rowmeta + (size_t)tile * kLprRows + 64 * w,
-                      sp.cnt + wt, sp.cols + wt * sp.cstride, reinterpret_cast<T*>(sp.vals) + wt * sp.slot);
+                      sp.cnt + wt, sp.cols + wt * sp.slot, reinterpret_cast<T*>(sp.vals) + wt * sp.slot);
 }
 
 
-// ---- fused copy worker (see LprFuse): one wave, super-tiles in row order until none is left
-__device__ __forceinline__ uint32_t ld_sc1(const void* p) {  // global_load_dword sc1 (L1 bypassed)
-    return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename T>
-__device__ __forceinline__ T ld_sc1_t(const T* p) {
-    if constexpr (sizeof(T) == 4) {
-        return __uint_as_float(ld_sc1(p));
-    } else {
-        const uint32_t lo = ld_sc1(p), hi = ld_sc1(reinterpret_cast<const uint32_t*>(p) + 1);
-        return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-    }
-}
-template <typename T>
-__device__ __forceinline__ void fz_store(const LprFuse& fz, unsigned long long o, uint32_t col, T v) {
-    if (fz.oi64) reinterpret_cast<int64_t*>(fz.Cj)[o] = (int64_t)col;
-    else reinterpret_cast<int32_t*>(fz.Cj)[o] = (int32_t)col;
-    reinterpret_cast<T*>(fz.Cx)[o] = v;
-}
-__device__ __forceinline__ void fz_ptr(const LprFuse& fz, int64_t i, unsigned long long v) {
-    if (fz.op64) reinterpret_cast<int64_t*>(fz.Cp)[i] = (int64_t)v;
-    else reinterpret_cast<int32_t*>(fz.Cp)[i] = (int32_t)v;
-}
-template <typename T>
-__device__ void lpr_copy_worker(const LprSpace& sp, const LprFuse& fz, int64_t n_rows, unsigned n_tiles, int order,
-                                Workspace* ws) {
-    const int lane = threadIdx.x & 63;
-    const unsigned n_st = (n_tiles + kPartTiles - 1) / kPartTiles, n_units = 4 * n_tiles;
-    const unsigned long long base = *fz.base_in;  // final: written by the previous chunk's scan kernel
-    const T* vals = reinterpret_cast<const T*>(sp.vals);
-    const bool rev = order != RP_ORDER_SORTED;
-    while (true) {
-        unsigned s = 0;
-        if (lane == 0) s = atomicAdd(fz.ticket, 1u);
-        s = (unsigned)__builtin_amdgcn_readfirstlane((int)s);
-        if (s >= n_st) return;
-        const unsigned u0 = s * 4u * kPartTiles, u1 = std::min(u0 + 4u * kPartTiles, n_units);
-        unsigned long long a = 0;
-        for (long spins = 0;; ++spins) {  // every unit of the super-tile has signalled
-            a = __hip_atomic_load(&fz.ag[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((a >> 48) >= u1 - u0) break;
-            if (spins > kSpinLimit) {
-                if (lane == 0) atomicOr(&ws->error, 1u);
-                return;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if ((a >> 40) & 0xffu) {  // a heavy unit: its count is known only after the heavy kernels
-            if (lane == 0) __hip_atomic_store(&fz.st[s], kFlagP | kXVal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            continue;
-        }
-        const unsigned long long excl = lookback_wave(fz.st, s, a & ((1ull << 40) - 1), ws);
-        if (excl >= kXVal) continue;  // behind a heavy super-tile (its prefix published >= kXVal too)
-        unsigned long long G = base + excl;
-        for (unsigned rb = u0; rb < u1; ++rb) {
-            const int64_t row0 = (int64_t)rb * 64;
-            if (row0 >= n_rows) break;  // the last tile's empty units
-            const int nrows = (int)std::min<int64_t>(64, n_rows - row0);
-            const uint32_t meta = lane < nrows ? ld_sc1(sp.rowmeta + row0 + lane) : 0u;
-            const uint32_t kst = meta & 0xffffu, kept = meta >> 16;
-            const uint32_t incl = wave_scan_dpp(kept), pre = incl - kept;
-            const uint32_t cnt = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            if (lane < nrows) fz_ptr(fz, row0 + lane, G + pre);
-            if (G + cnt <= fz.capacity) {
-                const uint16_t* __restrict__ sc = sp.cols + (size_t)rb * sp.cstride;
-                const T* __restrict__ sv = vals + (size_t)rb * sp.slot;
-                if (lpr_slot_final(kept, kst, pre)) {  // one run in final order: 8 outputs per lane
-                    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)sc, (short)0, (int)(2 * sp.slot), 0x00020000);
-                    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)sv, (short)0, (int)(sizeof(T) * sp.slot), 0x00020000);
-                    for (uint32_t o0 = 8 * lane; o0 < cnt; o0 += 512) {
-                        const v4u cw = __builtin_amdgcn_raw_buffer_load_b128(rc, 2 * o0, 0, kAuxSC1);
-                        T xv[8];
-                        if constexpr (sizeof(T) == 4) {
-                            const v4u a0 = __builtin_amdgcn_raw_buffer_load_b128(rv, 4 * o0, 0, kAuxSC1);
-                            const v4u a1 = __builtin_amdgcn_raw_buffer_load_b128(rv, 4 * o0 + 16, 0, kAuxSC1);
-#pragma unroll
-                            for (int k = 0; k < 4; ++k) {
-                                xv[k] = __uint_as_float(a0[k]);
-                                xv[4 + k] = __uint_as_float(a1[k]);
-                            }
-                        } else {
-#pragma unroll
-                            for (int h = 0; h < 4; ++h) {
-                                const v4u a0 = __builtin_amdgcn_raw_buffer_load_b128(rv, 8 * o0 + 16 * h, 0, kAuxSC1);
-                                xv[2 * h] = __longlong_as_double((long long)(((uint64_t)a0[1] << 32) | a0[0]));
-                                xv[2 * h + 1] = __longlong_as_double((long long)(((uint64_t)a0[3] << 32) | a0[2]));
-                            }
-                        }
-#pragma unroll
-                        for (int k = 0; k < 8; ++k)
-                            if (o0 + k < cnt) fz_store<T>(fz, G + o0 + k, (cw[k >> 1] >> (16 * (k & 1))) & 0xffffu, xv[k]);
-                    }
-                } else {  // rows built with gaps (exact path): each output finds its row
-                    const uint32_t rbase = rev ? kst + kept - 1 : kst;
-                    for (uint32_t o = lane; __ballot(o < cnt); o += 64) {
-                        int lo = 0;
-#pragma unroll
-                        for (int step = 32; step > 0; step >>= 1) {
-                            const uint32_t pv = (uint32_t)__shfl((int)pre, lo + step, 64);
-                            if (lo + step < 64 && pv <= o) lo += step;
-                        }
-                        const uint32_t i = o - (uint32_t)__shfl((int)pre, lo, 64);
-                        const uint32_t b = (uint32_t)__shfl((int)rbase, lo, 64);
-                        if (o < cnt) {
-                            const uint32_t src = std::min(rev ? b - i : b + i, sp.slot - 1);
-                            const uint32_t cw = ld_sc1(sc + (src & ~1u));
-                            fz_store<T>(fz, G + o, (cw >> (16 * (src & 1))) & 0xffffu, ld_sc1_t<T>(sv + src));
-                        }
-                    }
-                }
-            }
-            G += cnt;
-        }
-        if ((int64_t)u1 * 64 >= n_rows && lane == 0) fz_ptr(fz, n_rows, G);  // the chunk's last row ends here
-        if (lane == 0) fz.placed[s] = 1u;
-    }
-}
 // ------------------------------------------------------------------------------------------
 // Staged row-lane wave kernel, the uniform-column default: one 64-thread
 // workgroup = one wave = one 64-row unit, independent of every other wave (no block barrier, full
@@ -1928,7 +1773,7 @@ template <typename T, typename IP, int WPE = std::is_same<T, float>::value ? 7 :
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
                 const T* __restrict__ Ax, LprStage stg, int cap_a, uint32_t ucap, unsigned n_tiles, unsigned s8,
-                int order, LprSpace sp, Workspace* ws, LprFuse fz) {
+                int order, LprSpace sp, Workspace* ws) {
     extern __shared__ __align__(16) unsigned char lds[];  // region A (descriptors, then slot), region B
     __shared__ uint64_t s_flag[kWaveSteps];               // row-start bitmap over the unit's entries
     __shared__ uint64_t s_susp;                           // rows flagged for the exact path
@@ -1938,34 +1783,14 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     __shared__ T s_sfx[kWaveSide];                        // ... its value
     __shared__ uint32_t s_sfj[kWaveSide];                 // ... its side-table index
     const int lane = threadIdx.x & 63;
-    if (blockIdx.x < fz.n_workers) {  // fused copy: the grid's first workgroups (dispatched first)
-        lpr_copy_worker<T>(sp, fz, n_rows, n_tiles, order, ws);
-        return;
-    }
-    const unsigned bid = blockIdx.x - fz.n_workers;  // n_workers is a multiple of 8: same XCD as bid
-    // Unit order. Unfused: the partition's XCD ranges, XCD x takes the units of super-tiles
-    // [x * s8, (x + 1) * s8) in order (workgroup i runs on XCD i % 8). Fused: super-tile s on XCD
-    // s % 8, all XCDs in row order together, so super-tiles complete about in row order (the
-    // workers' look-back follows the front); a super-tile's 8 units stay on one XCD either way.
-    static_assert(4 * kPartTiles == 8, "8 units per super-tile");
-    const unsigned rb = fz.n_workers ? 64u * ((bid >> 3) >> 3) + 8u * (bid & 7u) + ((bid >> 3) & 7u)
-                                     : (bid & 7u) * (4u * kPartTiles * s8) + (bid >> 3);
+    // unit order follows the partition's XCD ranges: XCD x takes the units of super-tiles
+    // [x * s8, (x + 1) * s8) in order (workgroup i runs on XCD i % 8)
+    const unsigned rb = (blockIdx.x & 7u) * (4u * kPartTiles * s8) + (blockIdx.x >> 3);
     if (rb >= 4 * n_tiles) return;
-    // the copy workers' hand-off: every store they read was sc1 (write-through) and has drained,
-    // then ONE agent-scope add per unit (MI355X_MICROARCH.md: hand-offs with sc1 loads)
-    auto signal = [&](uint32_t tot, bool heavy) {
-        if (!fz.n_workers) return;
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_fetch_add(&fz.ag[rb >> 3], (1ull << 48) + (heavy ? (1ull << 40) : (unsigned long long)tot),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
-    const int aux = fz.n_workers ? kAuxSC1 : kAuxNT;
     const unsigned tile = rb >> 2, u = rb & 3;
     const int64_t row0 = (int64_t)rb * 64;
     if (row0 >= n_rows) {  // the last tile's empty units
         if (lane == 0) sp.cnt[rb] = 0u;
-        signal(0, false);
         return;
     }
     const int nrows = (int)std::min<int64_t>(64, n_rows - row0);
@@ -2006,14 +1831,11 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     const uint32_t nu = E1 - E0, nsteps = (nu + 63) >> 6;
     if (tn > cap_a || nu > ucap) {  // uniform: the partition staged nothing / too many for the registers
         go_heavy();
-        signal(0, true);
         return;
     }
     if (nu == 0) {  // uniform: 64 empty rows (or fewer at the end): nothing to gather or store
-        const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)(sp.rowmeta + row0), (short)0, 256, 0x00020000);
-        st_b32(0u, rm, lane < nrows ? 4u * lane : 0x80000000u, aux);
+        if (lane < nrows) sp.rowmeta[row0 + lane] = 0u;
         if (lane == 0) sp.cnt[rb] = 0u;
-        signal(0, false);
         return;
     }
     const T* __restrict__ Axt = Ax + ta;
@@ -2047,7 +1869,6 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         }
         if (pos0 != nu) {  // uniform; cannot happen (the partition counted this tile): exact path
             go_heavy();
-            signal(0, true);
             return;
         }
         __builtin_amdgcn_wave_barrier();
@@ -2239,7 +2060,6 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     __builtin_amdgcn_wave_barrier();
     if (bad) {  // uniform
         go_heavy();
-        signal(0, true);
         return;
     }
     // ---- per row: kept count and a Bloom check of its columns (3 x 64-bit filters in registers)
@@ -2329,7 +2149,6 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     if (kst + kept > kend_r && nonempty) overflow = true;
     if (__ballot(overflow)) {  // this unit cannot finish on the fast path: the whole tile goes heavy
         go_heavy();
-        signal(0, true);
         return;
     }
     if (order == RP_ORDER_SORTED && kept > 1) {  // ascending columns inside the row's slot range
@@ -2347,10 +2166,8 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         }
     }
     __builtin_amdgcn_wave_barrier();
-    const uint32_t tot = lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, order, sp.rowmeta + row0,
-                                           sp.cnt + rb, sp.cols + (size_t)rb * sp.cstride,
-                                           reinterpret_cast<T*>(sp.vals) + (size_t)rb * sp.slot, aux);
-    signal(tot, false);
+    lpr_store_slot<T>(cb, vb, kst, kept, valid, lane, carry_k, order, sp.rowmeta + row0, sp.cnt + rb,
+                      sp.cols + (size_t)rb * sp.slot, reinterpret_cast<T*>(sp.vals) + (size_t)rb * sp.slot);
 }
 
 // heavy tiles, pass 0: the exact dense accumulator counts their rows (grid-stride over the list);
@@ -2449,12 +2266,11 @@ lpr_scan_kernel(LprSpace sp, size_t n, const unsigned long long* __restrict__ ba
 template <typename T, typename OP, typename OI>
 __global__ void __launch_bounds__(kBlock)
 lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ Cp, OI* __restrict__ Cj,
-                T* __restrict__ Cx, unsigned long long capacity, int order, const uint32_t* __restrict__ placed) {
+                T* __restrict__ Cx, unsigned long long capacity, int order) {
     const T* vals = reinterpret_cast<const T*>(sp.vals);
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (unsigned tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         if (sp.tflag[tile]) continue;  // lpr_heavy_write_kernel places it
-        if (placed && placed[tile / kPartTiles]) continue;  // the fused copy workers placed it
         const size_t wt = (size_t)tile * 4 + w;
         const unsigned long long G = sp.off[wt];
         const uint32_t cnt = sp.cnt[wt];
@@ -2467,7 +2283,7 @@ lpr_copy_kernel(LprSpace sp, int64_t n_rows, unsigned n_tiles, OP* __restrict__ 
         if (r < nrows) Cp[row0 + r] = (OP)(G + pre);
         if (tile == n_tiles - 1 && threadIdx.x == kBlock - 1) Cp[n_rows] = (OP)(G + cnt);
         if (G + cnt > capacity) continue;
-        const uint16_t* __restrict__ sc = sp.cols + wt * sp.cstride;
+        const uint16_t* __restrict__ sc = sp.cols + wt * sp.slot;
         const T* __restrict__ sv = vals + wt * sp.slot;
         constexpr int kCopyU = 8;
         if (lpr_slot_final(kept, kst, pre)) {  // stored in final order (lpr_store_slot): one run
@@ -2702,7 +2518,6 @@ struct rp_projector {
     int opt_defer_ticks = -1;   // -1 default
     int64_t opt_chunk_rows = 0; // 0 default
     int opt_host_threads = -1;  // -1 default
-    int opt_fused_copy = -1;    // -1 default (off), 0 off, 1 on: copy workers in the staged wave kernel
     // the last stream call (rp_project_stream / rp_libsvm_project_stream): chunks, chunks recomputed
     // after the pipeline (their output outgrew the device slot), slot regrowths in the pipeline
     int64_t st_chunks = 0, st_redo = 0, st_regrow = 0;
@@ -2773,7 +2588,6 @@ struct Plan {
     size_t lcnt = 0, loff = 0, lhl = 0, ltf = 0, lrow = 0, lcols = 0, lvals = 0;
     size_t off2 = 0, gb = 0, fill = 0;  // staged runs (lpr_reserve_kernel, lpr_partition_kernel)
     int64_t sd_words = 0;               // S / D capacity (words)
-    size_t fag = 0, fst = 0, fpl = 0, ftk = 0, fz_bytes = 0;  // fused copy (LprFuse), zeroed per chunk
     unsigned groups = 0;
     uint32_t ucap = 0;                  // staged: entries per 64-row unit on the fast path (<= 16 steps)
 };
@@ -2844,7 +2658,7 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
         pl.lhl = pl.loff + al(8 * nw);
         pl.lrow = pl.lhl + al(4 * (size_t)pl.n_tiles);
         pl.lcols = pl.lrow + al(4 * (size_t)kLprRows * (size_t)pl.n_tiles);
-        pl.lvals = pl.lcols + al(2 * (size_t)lpr_cstride(pl.lpr_slot) * nw);
+        pl.lvals = pl.lcols + al(2 * (size_t)pl.lpr_slot * nw);
         pl.total = pl.lvals + al((size_t)vs * (size_t)pl.lpr_slot * nw);
         const bool want_stage = h->stage_mode == 1 || (h->stage_mode == -1 && kLprStageAuto &&
                                                        nnz_a >= kStageMinNnz && 8 * h->m >= kStageMinTable);
@@ -2883,14 +2697,6 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
                 pl.s = pl.fill + al(4 * nseg);
                 pl.d = pl.s + al(4 * sd);
                 pl.total = pl.d + al(4 * sd);
-                // fused copy (LprFuse): per super-tile ag, st (8 B), placed (4 B), then the ticket
-                const size_t nst = (size_t)(pl.n_tiles + kPartTiles - 1) / kPartTiles;
-                pl.fag = pl.total;
-                pl.fst = pl.fag + al(8 * nst);
-                pl.fpl = pl.fst + al(8 * nst);
-                pl.ftk = pl.fpl + al(4 * nst);
-                pl.total = pl.ftk + 256;
-                pl.fz_bytes = pl.total - pl.fag;
             }
         }
         return pl;
@@ -2985,14 +2791,11 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
                 reinterpret_cast<uint32_t*>(base + pl.lhl), reinterpret_cast<uint32_t*>(base + pl.ltf),
                 reinterpret_cast<uint32_t*>(base + pl.lrow), reinterpret_cast<uint16_t*>(base + pl.lcols),
                 reinterpret_cast<unsigned char*>(base + pl.lvals), reinterpret_cast<unsigned long long*>(ws + 1),
-                pl.lpr_slot, lpr_cstride(pl.lpr_slot)};
+                pl.lpr_slot};
     const unsigned n_tiles = (unsigned)((a->n_rows + kLprRows - 1) / kLprRows);
     const IP* Ap = (const IP*)a->indptr;
     const T* Ax = (const T*)a->data;
     const unsigned t8 = (n_tiles + 7) / 8;
-    // copy workers fused into the staged wave kernel (LprFuse; RP_OPT_FUSED_COPY)
-    const bool fused = staged && h->opt_fused_copy == 1;
-    LprFuse fz{};
     if (staged) {
         // the gate word: 1 unless a segment overflow in a partition (this chunk's or an earlier
         // one's) cleared it; the wave kernel then gathers directly
@@ -3025,24 +2828,9 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
         const size_t wlds = lpr_wave_lds_bytes(pl.lpr_slot, sizeof(T), pl.ucap, pl.nb);
         HIP_TRY(hipFuncSetAttribute((const void*)lpr_wave_kernel<T, IP>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)wlds));
-        if (fused) {
-            HIP_TRY(hipMemsetAsync(base + pl.fag, 0, pl.fz_bytes, st));
-            fz.ag = reinterpret_cast<unsigned long long*>(base + pl.fag);
-            fz.st = reinterpret_cast<unsigned long long*>(base + pl.fst);
-            fz.placed = reinterpret_cast<uint32_t*>(base + pl.fpl);
-            fz.ticket = reinterpret_cast<unsigned int*>(base + pl.ftk);
-            fz.base_in = carry + (chunk & 1);
-            fz.Cp = c->indptr;
-            fz.Cj = c->indices;
-            fz.Cx = c->data;
-            fz.capacity = (unsigned long long)c->capacity;
-            fz.n_workers = kFuseWorkers;
-            fz.op64 = std::is_same<OP, int64_t>::value;
-            fz.oi64 = std::is_same<OI, int64_t>::value;
-        }
-        hipLaunchKernelGGL((lpr_wave_kernel<T, IP>), dim3(8u * 4u * kPartTiles * s8 + fz.n_workers), dim3(64), wlds,
+        hipLaunchKernelGGL((lpr_wave_kernel<T, IP>), dim3(8u * 4u * kPartTiles * s8), dim3(64), wlds,
                            st, R, mag, a->n_rows, Ap, a->indices, Ax, stg, pl.caps.cap_a, pl.ucap, n_tiles, s8, order,
-                           sp, ws, fz);
+                           sp, ws);
     } else {
         const size_t lds = lpr_lds_bytes(pl.caps.cap_a, sizeof(T), pl.lpr_slot);
         const void* fn = (const void*)lpr_main_flat_kernel<T, IP>;
@@ -3065,7 +2853,7 @@ int launch_lpr_chunk(const PackedR& R, T mag, rp_projector* h, const rp_csr_in* 
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL((lpr_copy_kernel<T, OP, OI>), dim3(std::min<unsigned>(n_tiles, 1u << 20)), dim3(kBlock), 0, st,
                        sp, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices, (T*)c->data,
-                       (unsigned long long)c->capacity, order, fused ? (const uint32_t*)fz.placed : nullptr);
+                       (unsigned long long)c->capacity, order);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipFuncSetAttribute((const void*)lpr_heavy_write_kernel<T, IP, OP, OI>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl));
@@ -3688,10 +3476,7 @@ int rp_projector_set_option(rp_projector* h, int32_t option, int64_t value) {
         case RP_OPT_HOST_THREADS:
             h->opt_host_threads = (int)std::max<int64_t>(std::min<int64_t>(value, 256), -1);
             return RP_OK;
-        case RP_OPT_FUSED_COPY:
-            if (value < -1 || value > 1) return fail(RP_ERR_INVALID, "fused copy must be -1 (default), 0 or 1");
-            h->opt_fused_copy = (int)value;
-            return RP_OK;
+
         default:
             return fail(RP_ERR_INVALID, "unknown option %d", option);
     }
@@ -3705,7 +3490,6 @@ int rp_projector_get_option(const rp_projector* h, int32_t option, int64_t* valu
         case RP_OPT_DEFER_TICKS: *value = h->opt_defer_ticks; return RP_OK;
         case RP_OPT_CHUNK_ROWS: *value = h->opt_chunk_rows; return RP_OK;
         case RP_OPT_HOST_THREADS: *value = h->opt_host_threads; return RP_OK;
-        case RP_OPT_FUSED_COPY: *value = h->opt_fused_copy; return RP_OK;
         default: return fail(RP_ERR_INVALID, "unknown option %d", option);
     }
 }

@@ -355,15 +355,14 @@ class Projector:
 
     _OPTIONS = {"pipeline": nat.RP_OPT_PIPELINE, "defer_polls": nat.RP_OPT_DEFER_POLLS,
                 "defer_ticks": nat.RP_OPT_DEFER_TICKS, "chunk_rows": nat.RP_OPT_CHUNK_ROWS,
-                "host_threads": nat.RP_OPT_HOST_THREADS, "fused_copy": nat.RP_OPT_FUSED_COPY}
-    _OPTION_DEFAULTS = {"pipeline": 0, "defer_polls": -2, "defer_ticks": -1, "chunk_rows": 0, "host_threads": -1,
-                        "fused_copy": -1}
+                "host_threads": nat.RP_OPT_HOST_THREADS}
+    _OPTION_DEFAULTS = {"pipeline": 0, "defer_polls": -2, "defer_ticks": -1, "chunk_rows": 0, "host_threads": -1}
     _PIPELINES = {"auto": 0, "tile": 1, "rowlane": 2}
 
     def set_option(self, name: str, value):
         """Tuning / test option of this projector (rp_projector_set_option; results are identical
         under every setting): pipeline ("auto" | "tile" | "rowlane"), defer_polls, defer_ticks,
-        chunk_rows, host_threads, fused_copy (-1 default / 0 / 1); ``None`` restores the default."""
+        chunk_rows, host_threads; ``None`` restores the default."""
         if name not in self._OPTIONS:
             raise ValueError(f"unknown option {name!r}; one of {sorted(self._OPTIONS)}")
         if value is None:

@@ -200,11 +200,10 @@ def test_rowlane_chunked_launch_vs_oracle(R2m_p1k, chunk):
                    kdd_like(rng, 123_321 if chunk == "50000" else 3001, m, powerlaw=True, values="normal")]).tocsr()
     want = oracle_product(A, R)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
-    for stage, fused in (("off", -1), ("on", -1), ("on", 0)):
+    for stage in ("off", "on"):
         P = Projector(R)
         P.set_option("pipeline", "rowlane")
         P.set_option("chunk_rows", int(chunk))
-        P.set_option("fused_copy", fused)
         P.set_staging(stage, 19)
         assert P.plan(A.shape[0], A.nnz) == {"pipeline": "rowlane", "staged": stage == "on",
                                              "bucket_shift": 19 if stage == "on" else 0}
@@ -277,23 +276,16 @@ def _rows(rng, k, pool, m, dtype=np.float32):
                           np.concatenate([[0], np.cumsum(k)])), shape=(n, m))
 
 
-def _check_rowlane_staged(R, A, shift, staged=True, fused=(-1, 0)):
+def _check_rowlane_staged(R, A, shift, staged=True):
     """Row-lane pipeline with staging forced on: host path in both orders against the oracle, then
     the device path, whose workspace records whether the staged gather ran (`staged`) or a segment
-    past its reserve sent the call to direct gathers. Each with the copy workers fused into the wave
-    kernel (default) and with the copy kernel alone (option fused_copy 0)."""
-    for fz in fused:
-        _check_rowlane_staged_one(R, A, shift, staged, fz)
-
-
-def _check_rowlane_staged_one(R, A, shift, staged, fused):
+    past its reserve sent the call to direct gathers."""
     import torch
 
     want = oracle_product(A, R)
     Cj, Cx = smmp.sorted_rows(want[0], want[1], want[2])
     P = Projector(R)
     P.set_option("pipeline", "rowlane")
-    P.set_option("fused_copy", fused)
     P.set_staging("on", shift)
     assert P.plan(A.shape[0], A.nnz) == {"pipeline": "rowlane", "staged": True, "bucket_shift": shift}
     assert_same_csr(P.matmul(A), *want)
