@@ -1276,6 +1276,25 @@ __device__ __forceinline__ bool lpr_bloom(const uint16_t* cb, uint32_t kst, uint
     return hit;
 }
 
+// Exact repeat check of one row's slot range [kst, kst + n) (the staged wave kernel): every pair of
+// its first 16 columns compared in registers (120 compares, straight-line, no false alarms: ~1/3
+// of the Bloom check's VALU, which also flagged ~1% of the rows for nothing); a row of more than 16
+// products is flagged (the exact path handles it). Columns past n are distinct sentinels.
+__device__ __forceinline__ bool lpr_repeat16(const uint16_t* cb, uint32_t kst, uint32_t n, uint32_t lim) {
+    uint32_t c[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t v = cb[std::min(kst + (uint32_t)i, lim)];
+        c[i] = (uint32_t)i < n ? v : 0x10000u + (uint32_t)i;
+    }
+    bool rep = n > 16;
+#pragma unroll
+    for (int i = 1; i < 16; ++i)
+#pragma unroll
+        for (int j = 0; j < i; ++j) rep |= c[i] == c[j];
+    return rep;
+}
+
 // A wave's slot to HBM (row r's kept entries at [kst, kst + kept), in first-touch order, or
 // ascending for RP_ORDER_SORTED): `extent` entries copied coalesced, each row's (kst, kept) in
 // rowmeta, the run's entry count in *cnt. A slot without gaps (every row with entries starts at
@@ -2070,7 +2089,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     const uint32_t kend_r = nx < 64 ? kst_next : carry_k;
     uint32_t kept = nonempty ? kend_r - kst : 0u;
     bool hit = false;
-    if (!overflow) hit = lpr_bloom(cb, kst, kept);
+    if (!overflow) hit = lpr_repeat16(cb, kst, kept, sp.slot + 1);
     const uint64_t susp = s_susp;
     uint64_t todo = susp | __ballot(hit);  // lane == row within the unit
     if (__ballot(overflow)) todo = 0;
@@ -2093,11 +2112,9 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         for (uint32_t e0 = a0; !from_slot && e0 < a1; e0 += 64) {
             const uint32_t e = e0 + lane;
             const bool in = e < a1;
-            // entries [e0, e0 + 64) lie in steps x0 = (e0 - E0) / 64 and x0 + 1
-            const uint32_t x0 = (e0 - E0) >> 6, src = (e - E0) & 63;
-            const uint32_t d0 = __shfl((int)reg_pick(dv, x0), (int)src, 64);
-            const uint32_t d1 = __shfl((int)reg_pick(dv, std::min(x0 + 1, (uint32_t)kWaveSteps - 1)), (int)src, 64);
-            const uint32_t d = in ? (((e - E0) >> 6) == x0 ? d0 : d1) : 0u;
+            // the entry's W32 word gathered again (rows with a zero value are rare; the unit's
+            // descriptors are not kept in registers past the flat pass)
+            const uint32_t d = in ? stg.w32[Aj[ta + e]] : 0u;
             const T x = in ? Axt[e] : T(0);
             const uint32_t np = in ? ((d >> 30) < 3 ? (d >> 30) : (d >> 26) & 15u) : 0u;
             const uint32_t inc = wave_scan_dpp(np);
