@@ -1758,7 +1758,8 @@ __host__ __device__ inline size_t lpr_wave_region_a(uint32_t slot, size_t vs, ui
     return std::max(s, 4 * (size_t)ucap);
 }
 __host__ __device__ inline size_t lpr_wave_lds_bytes(uint32_t slot, size_t vs, uint32_t ucap, int nb) {
-    const size_t scr = ((2 * (size_t)kWaveScr + 15) & ~size_t(15)) + vs * kWaveScr;
+    const size_t scr = std::max(((2 * (size_t)kWaveScr + 15) & ~size_t(15)) + vs * kWaveScr,
+                                (2 + vs + 4) * (size_t)kWaveSide);  // exact scratch / side list
     const size_t tab = (8 * (size_t)kWaveSteps + 4 * (size_t)std::max(nb, 1) + 15) & ~size_t(15);
     // a multiple of 16 bytes: the next wave's regions (8-byte bitmap words, f64 values) stay aligned
     return lpr_wave_region_a(slot, vs, ucap) + std::max(scr, tab);
@@ -1788,7 +1789,10 @@ __device__ __forceinline__ uint32_t reg_pick(const uint32_t (&v)[N], uint32_t x)
 // allows ~29 one-wave workgroups per CU anyway; 8 waves in 64 VGPRs measured slower, §3d); f64
 // unconstrained. One wave per workgroup, each its own unit, no block barrier (a super-tile's 8 units
 // in one workgroup measured slower too: 25.6 vs 18.3 ms, §3d).
-template <typename T, typename IP, int WPE = std::is_same<T, float>::value ? 7 : 1>
+#ifndef RP_WAVE_WPE
+#define RP_WAVE_WPE 7
+#endif
+template <typename T, typename IP, int WPE = std::is_same<T, float>::value ? RP_WAVE_WPE : 1>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE)))
 lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
                 const T* __restrict__ Ax, LprStage stg, int cap_a, uint32_t ucap, unsigned n_tiles, unsigned s8,
@@ -1798,9 +1802,6 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     __shared__ uint64_t s_susp;                           // rows flagged for the exact path
     __shared__ uint16_t s_kst[64];
     __shared__ uint8_t s_nz2row[64];
-    __shared__ uint16_t s_sfk[kWaveSide];                 // side entry's slot position (0xffff: zero x)
-    __shared__ T s_sfx[kWaveSide];                        // ... its value
-    __shared__ uint32_t s_sfj[kWaveSide];                 // ... its side-table index
     const int lane = threadIdx.x & 63;
     // unit order follows the partition's XCD ranges: XCD x takes the units of super-tiles
     // [x * s8, (x + 1) * s8) in order (workgroup i runs on XCD i % 8)
@@ -1863,6 +1864,11 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
     T xv[kWaveSteps];  // lanes past the unit hold any value: their descriptors are 0 (no products)
     uint32_t* desc = reinterpret_cast<uint32_t*>(lds);
     const size_t ra = lpr_wave_region_a(sp.slot, sizeof(T), ucap);
+    // the side list (written from the side pre-pass to the side fill) in region B: the run lookup
+    // there is dead once the S/D loads are issued, the exact-path scratch is used only after it
+    uint16_t* s_sfk = reinterpret_cast<uint16_t*>(lds + ra);                      // slot position (0xffff: zero x)
+    T* s_sfx = reinterpret_cast<T*>(lds + ra + 2 * kWaveSide);                     // ... its value
+    uint32_t* s_sfj = reinterpret_cast<uint32_t*>(lds + ra + (2 + sizeof(T)) * kWaveSide);  // side-table index
     constexpr int kW0 = 12;  // steps loaded unconditionally (KDD2012 units: 11-12); the rest if present
     if (staged) {
         // the unit's layout: runs in bucket order; run k (k-th nonempty bucket) starts at layout
@@ -1920,17 +1926,7 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
 #pragma unroll
             for (int x = kW0; x < kWaveSteps; ++x) sd_load(x);
         }
-        // each D word to its entry's place (lanes past the unit loaded the first word: skipped)
-#pragma unroll
-        for (int x = 0; x < kW0; ++x)
-            if (64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
-        if (nsteps > kW0) {  // uniform
-#pragma unroll
-            for (int x = kW0; x < kWaveSteps; ++x)
-                if (64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
-        }
-        // the values (after the S/D words: issued earlier they and the S/D words did not fit the
-        // register budget together)
+        // the values, in flight with the S/D words (one memory round trip for all three)
         // the unit's values as a buffer of nu entries: no clamp (a lane past the unit reads 0, no
         // memory access), the step offset folds into the instruction
         const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -1941,6 +1937,15 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         if (nsteps > kW0) {  // uniform
 #pragma unroll
             for (int x = kW0; x < kWaveSteps; ++x) xv[x] = ldx(x);
+        }
+        // each D word to its entry's place (lanes past the unit loaded the first word: skipped)
+#pragma unroll
+        for (int x = 0; x < kW0; ++x)
+            if (64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
+        if (nsteps > kW0) {  // uniform
+#pragma unroll
+            for (int x = kW0; x < kWaveSteps; ++x)
+                if (64u * x + lane < nu) desc[(sv[x] >> 20) - E0] = dv[x];
         }
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
