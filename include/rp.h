@@ -179,10 +179,11 @@ int rp_projector_set_staging(rp_projector* h, int32_t mode, int32_t bucket_shift
  * identical under every setting; only the schedule changes. value < default sentinel restores the
  * default.
  *   RP_OPT_PIPELINE      0 auto (default); 1 tile pipeline; 2 row-lane pipeline where it can run
- *   RP_OPT_DEFER_POLLS   tile pipeline: -2 default (time budget); -1 tiles never park their output;
- *                        n >= 0 park after n unsuccessful look-back polls (time budget off)
- *   RP_OPT_DEFER_TICKS   256-row tiles' look-back wait budget in s_memrealtime ticks (100 MHz):
- *                        -1 default (800 = 8 us); n >= 0 override
+ *   RP_OPT_DEFER_POLLS   tile pipeline: -1 no tile slots (every tile waits for its prefix from a
+ *                        decoupled look-back, then writes C itself); any other value (default -2):
+ *                        every tile writes its own slot, a scan + copy place the slots (round 6;
+ *                        the round-5 look-back deferral it replaced cost configs[3] 65 of 198 ms)
+ *   RP_OPT_DEFER_TICKS   accepted and ignored since round 6 (kept for the ABI)
  *   RP_OPT_CHUNK_ROWS    row-lane rows per launch sequence: 0 default (2^27), else rounded up to
  *                        whole 256-row tiles
  *   RP_OPT_HOST_THREADS  helper threads of the host result download: -1 default (min(4, cores));

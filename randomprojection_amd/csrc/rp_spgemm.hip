@@ -63,27 +63,31 @@ struct Workspace {              // device memory header; tile states follow at +
     unsigned int tile_counter;
     unsigned int error;
     unsigned long long total;
-    unsigned int n_deferred;    // tiles that parked their output in the pool (see defer below)
+    unsigned int n_deferred;    // heavy tiles listed (exact slow path after the main kernel)
     unsigned int staged_used;   // written last in a call: 1 = the staged gather ran (rp_project_choice)
-    unsigned long long pool_used;  // entries of the deferred-output pool handed out
-    unsigned long long pad[4];
+    unsigned long long pool_used;  // (unused)
+    unsigned long long pad[4];     // tile slots: [0] scan ticket, [1] zero (scan base), [2] scan total
 };
 
-// Deferred output: a tile whose exclusive prefix is not published within
-// `defer_polls` look-back polls does not wait: it takes exactly its entry count from a shared
-// pool (one atomic), parks its finished output there (columns u16, values T, in final order) and
-// its row offsets in its header, leaves its aggregate published, appends itself to the deferred
-// list and exits; defer_copy_kernel later resolves its prefix (every state is final then) and
-// copies the entries to their place. A tile that finds the pool exhausted waits instead. Waiting
-// tiles hold LDS and waves idle: measured 7.6 ms of 32.9 on configs[1] (direct gathers).
+// Tile slots: with the full workspace, no tile waits for its predecessors. Each
+// tile writes its finished output (columns u16, values T, in final order) to its own slot of
+// `slot` entries (= cap_p, the tile's product cap: a bound on its outputs) and its row offsets to
+// its header; a scan of the tiles' counts gives their offsets and slot_copy_kernel moves every
+// slot to C. A tile past the caps (exact slow path) only counts, lists itself and marks its
+// header; tile_heavy_write_kernel writes it after the scan. (Round 5 published prefixes by a
+// decoupled look-back and parked late tiles in a pool: 55 ms of configs[3]'s 198 went to the
+// look-back and 10 ms to the pool copy.) cols == NULL: no slots (a small caller workspace), every
+// tile waits for its prefix (blocking look-back) and writes C itself.
 struct DeferSpace {
-    unsigned int* list;          // n_tiles
-    unsigned long long* pofs;    // n_tiles: pool offset of a deferred tile
-    uint16_t* hdr;               // n_tiles x (rpt + 1): row offsets, [rows] = count
-    uint16_t* cols;              // pool_cap
-    unsigned char* vals;         // pool_cap x sizeof(T)
-    unsigned long long pool_cap;
+    unsigned int* list;          // n_tiles: heavy tiles, count in ws->n_deferred
+    unsigned long long* toff;    // n_tiles: the tile's output offset (scan of tcnt)
+    uint16_t* hdr;               // n_tiles x (rpt + 1): row offsets in the tile, [rows] = count (0xffff: heavy)
+    uint16_t* cols;              // n_tiles x slot, or NULL
+    unsigned char* vals;         // n_tiles x slot x sizeof(T)
+    uint32_t* tcnt;              // n_tiles: the tile's output entries
+    unsigned long long slot;     // entries per tile slot
 };
+constexpr uint16_t kHdrHeavy = 0xffffu;
 
 // ------------------------------------------------------------------------------------------
 // R layouts
@@ -471,7 +475,7 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                        const int32_t* __restrict__ Aj, const T* __restrict__ Ax,
                        OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
                        unsigned long long capacity, Caps caps, int order, Workspace* ws,
-                       unsigned int n_tiles, DeferSpace dfr, int defer_polls, int defer_ticks) {
+                       unsigned int n_tiles, DeferSpace dfr) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ uint16_t s_rowptr[kBlock + 1];  // row -> first entry (tile-relative, <= cap_a)
     __shared__ uint16_t s_rowS[kBlock + 1];    // row -> first product
@@ -619,6 +623,12 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     const uint4* pk4 = reinterpret_cast<const uint4*>(s_pkr);
                     const uint32_t gq = q >> 2, oq = q & 3u;
                     bool leader = true;
+#ifdef RP_PROBE_NOSTAGE2  // timing probe only (wrong results): every product leads its own group
+                    if (true) {
+                        s_rank[q] = 1;
+                        continue;
+                    }
+#endif
                     for (uint32_t g = rs >> 2; g < gq; ++g) {
                         const uint4 k4 = pk4[g];
                         leader &= (k4.x != kr) & (k4.y != kr) & (k4.z != kr) & (k4.w != kr);
@@ -649,36 +659,27 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     s_rank[q] = flag;
                 }
                 __syncthreads();
-                // ---- stage 3: ranks of kept entries = tile-local output positions; look-back
+                // ---- stage 3: ranks of kept entries = tile-local output positions; the tile's slot
+                // (or, without slots, its prefix from a blocking look-back)
                 const uint32_t tile_c = lds_excl_scan(s_rank, P_t, s_wsum);
-                if (tid < 64) {
-                    const unsigned long long g =
-                        lookback_wave(states, tile, tile_c, ws, defer_polls, true, defer_ticks);
-                    if (tid == 0) s_off = g;
-                }
-                __syncthreads();
-                if (s_off == ~0ull) {  // uniform: no prefix yet -> take pool space, or wait
-                    if (tid == 0) {
-                        const unsigned long long o = atomicAdd(&ws->pool_used, (unsigned long long)tile_c);
-                        s_pool = o + tile_c <= dfr.pool_cap ? o : ~0ull;
-                        if (s_pool != ~0ull) {
-                            dfr.pofs[tile] = o;
-                            dfr.list[atomicAdd(&ws->n_deferred, 1u)] = tile;
-                        }
+                const bool deferred = dfr.cols != nullptr;  // uniform: slots
+                if (deferred) {
+                    if (tid == 0) dfr.tcnt[tile] = tile_c;
+                    s_pool = (unsigned long long)tile * dfr.slot;
+                } else {
+                    if (tid < 64) {
+#ifdef RP_PROBE_NOLOOKBACK  // timing probe only (wrong results): no look-back, every tile at 0
+                        if (tid == 0) s_off = 0;
+#else
+                        const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, true, 0);
+                        if (tid == 0) s_off = g;
+#endif
                     }
                     __syncthreads();
-                    if (s_pool == ~0ull) {
-                        if (tid < 64) {
-                            const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, false, 0);
-                            if (tid == 0) s_off = g;
-                        }
-                        __syncthreads();
-                    }
                 }
-                const bool deferred = s_off == ~0ull;  // uniform
                 const unsigned long long G = deferred ? 0ull : s_off;
-                // deferred: entries go to the pool at their tile-local positions and the row offsets
-                // to the tile's header; defer_copy_kernel adds the prefix later
+                // slots: entries go to the tile's slot at their tile-local positions and the row
+                // offsets to its header; slot_copy_kernel adds the offset after the scan
                 if (deferred) {
                     uint16_t* ro = dfr.hdr + (size_t)tile * (caps.rpt + 1);
                     if (tid < nrows) ro[tid] = s_rank[s_rowS[tid]];
@@ -727,6 +728,14 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                                   Cp, Cj, Cx, false, order);
     uint32_t tile_c;
     (void)block_excl_scan(tid < nrows ? s_rowc[tid] : 0u, s_wsum, &tile_c);
+    if (dfr.cols) {  // slots: count only; tile_heavy_write_kernel writes it after the scan
+        if (tid == 0) {
+            dfr.tcnt[tile] = tile_c;
+            dfr.hdr[(size_t)tile * (caps.rpt + 1) + nrows] = kHdrHeavy;
+            dfr.list[atomicAdd(&ws->n_deferred, 1u)] = tile;
+        }
+        return;
+    }
     if (tid < 64) {
         const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, true, 0);
         if (tid == 0) s_off = g;
@@ -1172,41 +1181,68 @@ lpr_gather_kernel(const uint32_t* __restrict__ W32, const uint32_t* __restrict__
     }
 }
 
-// Deferred tiles: prefix from the (now final) look-back states, then the parked slot is copied to
-// its place. Grid-stride over the deferred list; every state is published when this runs.
+// Tile slots to C after the scan of the tiles' counts (DeferSpace): grid-stride over the tiles;
+// heavy tiles are written by tile_heavy_write_kernel.
 template <typename T, typename OP, typename OI>
 __global__ void __launch_bounds__(kBlock)
-defer_copy_kernel(DeferSpace dfr, Workspace* ws, Caps caps, int64_t n_rows, unsigned n_tiles,
-                  OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
-                  unsigned long long capacity) {
-    __shared__ unsigned long long s_g;
-    unsigned long long* states = reinterpret_cast<unsigned long long*>(ws + 1);
-    const unsigned nd = ws->n_deferred;
+slot_copy_kernel(DeferSpace dfr, Caps caps, int64_t n_rows, unsigned n_tiles, OP* __restrict__ Cp,
+                 OI* __restrict__ Cj, T* __restrict__ Cx, unsigned long long capacity) {
     const int tid = threadIdx.x;
     const T* vals = reinterpret_cast<const T*>(dfr.vals);
-    for (unsigned i = blockIdx.x; i < nd; i += gridDim.x) {
-        const unsigned tile = dfr.list[i];
+    for (unsigned tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const uint16_t* ro = dfr.hdr + (size_t)tile * (caps.rpt + 1);
         const int64_t row0 = (int64_t)tile * caps.rpt;
         const int nrows = (int)std::min<int64_t>(caps.rpt, n_rows - row0);
-        const uint32_t cnt = ro[nrows];
-        const unsigned long long po = dfr.pofs[tile];
-        if (tid < 64) {
-            const unsigned long long g = lookback_wave(states, tile, cnt, ws, -1, false);
-            if (tid == 0) s_g = g;
-        }
-        __syncthreads();
-        const unsigned long long G = s_g;
+        const unsigned long long G = dfr.toff[tile];
+        const uint32_t cnt = dfr.tcnt[tile];
+        if (tile == n_tiles - 1 && tid == 0) Cp[n_rows] = (OP)(G + cnt);
+        if (ro[nrows] == kHdrHeavy) continue;  // uniform
         for (int r = tid; r < nrows; r += kBlock) Cp[row0 + r] = (OP)(G + ro[r]);
-        if (G + cnt <= capacity)
-            for (uint32_t q = tid; q < cnt; q += kBlock) {
-                Cj[G + q] = (OI)dfr.cols[po + q];
-                Cx[G + q] = vals[po + q];
+        if (G + cnt <= capacity) {  // four entries per thread loaded before any is stored
+            const uint16_t* __restrict__ sc = dfr.cols + (size_t)tile * dfr.slot;
+            const T* __restrict__ sv = vals + (size_t)tile * dfr.slot;
+            constexpr int kU = 4;
+            for (uint32_t q0 = 0; q0 < cnt; q0 += kU * kBlock) {
+                uint16_t cv[kU];
+                T xv[kU];
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const uint32_t q = std::min(q0 + u * kBlock + tid, cnt - 1);
+                    cv[u] = __builtin_nontemporal_load(sc + q);
+                    xv[u] = __builtin_nontemporal_load(sv + q);
+                }
+#pragma unroll
+                for (int u = 0; u < kU; ++u) {
+                    const uint32_t q = q0 + u * kBlock + tid;
+                    if (q < cnt) {
+                        Cj[G + q] = (OI)cv[u];
+                        Cx[G + q] = xv[u];
+                    }
+                }
             }
-        if (tile == n_tiles - 1 && tid == 0) {
-            Cp[n_rows] = (OP)(G + cnt);
-            ws->total = G + cnt;
         }
+    }
+}
+
+// Heavy tiles of the slot mode: the exact slow path counts again, then writes at the scanned offset.
+template <typename T, typename IP, typename OP, typename OI, typename RL>
+__global__ void __launch_bounds__(kBlock)
+tile_heavy_write_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict__ Ap, const int32_t* __restrict__ Aj,
+                        const T* __restrict__ Ax, OP* __restrict__ Cp, OI* __restrict__ Cj, T* __restrict__ Cx,
+                        unsigned long long capacity, Caps caps, int order, Workspace* ws, DeferSpace dfr) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    __shared__ uint32_t s_wsum[kBlock / 64];
+    const unsigned nh = ws->n_deferred;
+    uint32_t* s_rowc = reinterpret_cast<uint32_t*>(lds + heavy_lds_bytes(p, sizeof(T)) - 4 * kBlock);
+    for (unsigned i = blockIdx.x; i < nh; i += gridDim.x) {
+        const unsigned tile = dfr.list[i];
+        const int64_t row0 = (int64_t)tile * caps.rpt;
+        const int nrows = (int)std::min<int64_t>(caps.rpt, n_rows - row0);
+        const unsigned long long G = dfr.toff[tile];
+        heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 0, 0, Cp, Cj, Cx,
+                                      false, order);
+        heavy_tile<T, IP, OP, OI, RL>(R, mag, Ap, Aj, Ax, row0, nrows, p, lds, s_rowc, s_wsum, 1, G, Cp, Cj, Cx,
+                                      G + dfr.tcnt[tile] <= capacity, order);
         __syncthreads();
     }
 }
@@ -2536,8 +2572,8 @@ struct rp_projector {
     int stage_sb = 0;    // bucket = 2^sb features; 0 = auto
     // rp_projector_set_option (tuning and tests; the library reads no environment variables)
     int opt_pipeline = 0;       // 0 auto, 1 tile, 2 row-lane where it can run
-    int opt_defer_polls = -2;   // -2 default (time budget), -1 never defer, n >= 0 polls
-    int opt_defer_ticks = -1;   // -1 default
+    int opt_defer_polls = -2;   // tile pipeline: -1 no slots (every tile waits, then writes C); else slots
+    int opt_defer_ticks = -1;   // ignored since round 6 (kept for the ABI)
     int64_t opt_chunk_rows = 0; // 0 default
     int opt_host_threads = -1;  // -1 default
     // the last stream call (rp_project_stream / rp_libsvm_project_stream): chunks, chunks recomputed
@@ -2595,8 +2631,8 @@ struct Plan {
     bool defer = false;
     int sb = 0, nb = 0;
     uint32_t ostride = 0;
-    size_t head = 0, dlist = 0, pofs = 0, dhdr = 0, pcols = 0, pvals = 0, cu = 0, s = 0, d = 0;
-    unsigned long long pool_cap = 0;
+    size_t head = 0, dlist = 0, pofs = 0, dhdr = 0, pcols = 0, pvals = 0, tcnt = 0, cu = 0, s = 0, d = 0;
+    unsigned long long pool_cap = 0;  // tile pipeline: entries per tile slot
     size_t total = 0;
     // row-lane pipeline (lpr_*): tiles of kLprRows rows, every tile's output in a fixed slot
     bool lpr = false;
@@ -2614,10 +2650,7 @@ struct Plan {
     uint32_t ucap = 0;                  // staged: entries per 64-row unit on the fast path (<= 16 steps)
 };
 
-constexpr unsigned kDeferCopyGrid = 32768;  // copy workgroups (grid-stride over the deferred list)
-constexpr int kDeferPolls = 4;                 // polls before a 256-row tile defers (time budget off)
-constexpr int kDeferPollsShort = 8;            // ... and before a tile of fewer than 128 rows does
-constexpr int kDeferTicks = 800;               // 256-row tiles: wait budget, 8 us (defer_ticks_setting)
+constexpr unsigned kSlotCopyGrid = 1u << 20;  // slot copy workgroups (grid-stride over the tiles)
 constexpr int64_t kStageMinNnz = 1 << 22;      // auto: stage only launches this large
 // rp_project_stream's default chunk: configs[1] host CSR in/out measured 475 M rows/s with 4M-row
 // chunks, 544 M with 2M (shorter fill and drain of the upload/compute/download pipeline)
@@ -2728,41 +2761,19 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
     pl.head = al(sizeof(Workspace) + 8u * (size_t)std::max<int64_t>(pl.n_tiles, 1));
     pl.zero = pl.head;
     pl.total = pl.head;
-    if (pl.n_tiles > 0 && allow_defer && nnz_a >= 0) {  // deferred-output list, headers, pool
+    if (pl.n_tiles > 0 && allow_defer && nnz_a >= 0) {  // tile slots (DeferSpace): list, offsets, headers, slots
         pl.defer = true;
-        // pool: the expected products (>= outputs) + 2% + 64K entries; a tile finding it full waits
-        pl.pool_cap = (unsigned long long)(1.02 * ppe * (double)nnz_a) + 65536ull;
+        pl.pool_cap = (unsigned long long)pl.caps.cap_p;  // a tile's outputs <= its products <= cap_p
+        const size_t nt = (size_t)pl.n_tiles;
         pl.dlist = pl.total;
-        pl.pofs = pl.dlist + al(4 * (size_t)pl.n_tiles);
-        pl.dhdr = pl.pofs + al(8 * (size_t)pl.n_tiles);
-        pl.pcols = pl.dhdr + al(2 * (size_t)(pl.caps.rpt + 1) * (size_t)pl.n_tiles);
-        pl.pvals = pl.pcols + al(2 * (size_t)pl.pool_cap);
-        pl.total = pl.pvals + al((size_t)vs * (size_t)pl.pool_cap);
+        pl.pofs = pl.dlist + al(4 * nt);
+        pl.tcnt = pl.pofs + al(8 * nt);
+        pl.dhdr = pl.tcnt + al(4 * nt);
+        pl.pcols = pl.dhdr + al(2 * (size_t)(pl.caps.rpt + 1) * nt);
+        pl.pvals = pl.pcols + al(2 * (size_t)pl.pool_cap * nt);
+        pl.total = pl.pvals + al((size_t)vs * (size_t)pl.pool_cap * nt);
     }
     return pl;  // the tile pipeline gathers R's descriptors directly (its staged gather was removed)
-}
-
-// Polls before a tile defers. Measured optimum differs with the tile shape and the gather pattern
-// (DESIGN.md §3d): configs[1] uniform columns 2/3/4/5/6/8 polls 28.0/27.9/27.9/27.9/28.1/28.5 ms,
-// 32.7 waiting (random-gather latency varies widely); the same rows with power-law columns
-// 2/4/8/12/16 polls 22.6/21.5/20.1/19.6/19.6 ms, 19.8 waiting; configs[3] (29-row tiles of 100-nnz
-// rows hitting L2) 268 ms at 8, 285 waiting, 325 at 2. 4 for 256-row tiles is the best uniform
-// setting and 5% better than 2 on power-law rows.
-// 256-row tiles wait for their prefix up to a time budget (s_memrealtime ticks, 100 MHz) rather
-// than a poll count: a poll takes longer when the random gathers congest memory, so a time budget
-// waits fewer polls where predecessors are slow and more where they finish quickly. Measured
-// (DESIGN.md §3d): 8 us gives configs[1] uniform 27.95 ms (polls: 27.9 at best) and power-law
-// 19.4 ms (polls 4: 21.0, never deferring: 19.8); 12 us already costs uniform 29.1 ms.
-// RP_OPT_DEFER_POLLS (tests, tuning) turns the time budget off; RP_OPT_DEFER_TICKS overrides it.
-int defer_ticks_setting(const rp_projector* h, const Caps& caps) {
-    if (h->opt_defer_ticks >= 0) return h->opt_defer_ticks;
-    if (h->opt_defer_polls >= -1) return 0;
-    return caps.rpt >= 128 ? kDeferTicks : 0;
-}
-
-int defer_polls_setting(const rp_projector* h, const Caps& caps) {
-    if (h->opt_defer_polls >= -1) return h->opt_defer_polls;  // -1 never defer, 0 defer at once
-    return caps.rpt >= 128 ? kDeferPolls : kDeferPollsShort;
 }
 
 template <typename T, typename IP, typename OP, typename OI, typename RL, int WPE = 1>
@@ -2777,20 +2788,39 @@ int launch_main(const RL& R, T mag, rp_projector* h, const rp_csr_in* a, const r
     HIP_TRY(hipFuncSetAttribute((const void*)spgemm_lookback_kernel<T, IP, OP, OI, RL, WPE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     char* base = reinterpret_cast<char*>(ws);
+    // slots unless the workspace is small or RP_OPT_DEFER_POLLS = -1 (every tile waits, then writes C)
+    const bool slots = pl.defer && h->opt_defer_polls != -1;
     DeferSpace dfr{reinterpret_cast<unsigned int*>(base + pl.dlist),
                    reinterpret_cast<unsigned long long*>(base + pl.pofs),
-                   reinterpret_cast<uint16_t*>(base + pl.dhdr), reinterpret_cast<uint16_t*>(base + pl.pcols),
-                   reinterpret_cast<unsigned char*>(base + pl.pvals), pl.pool_cap};
+                   reinterpret_cast<uint16_t*>(base + pl.dhdr),
+                   slots ? reinterpret_cast<uint16_t*>(base + pl.pcols) : nullptr,
+                   reinterpret_cast<unsigned char*>(base + pl.pvals), reinterpret_cast<uint32_t*>(base + pl.tcnt),
+                   pl.pool_cap};
     hipLaunchKernelGGL((spgemm_lookback_kernel<T, IP, OP, OI, RL, WPE>), dim3(n_tiles), dim3(kBlock), lds, st,
                        R, mag, (int)h->p, a->n_rows,
                        (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
                        (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order,
-                       ws, n_tiles, dfr, pl.defer ? defer_polls_setting(h, pl.caps) : -1,
-                       pl.defer ? defer_ticks_setting(h, pl.caps) : 0);
+                       ws, n_tiles, dfr);
     HIP_TRY(hipGetLastError());
-    if (pl.defer) {
-        hipLaunchKernelGGL((defer_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, kDeferCopyGrid)), dim3(kBlock), 0,
-                           st, dfr, ws, pl.caps, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices,
+    if (slots) {
+        // the tiles' offsets: scan of tcnt (4096 per block, look-back over blocks; its states in
+        // the tile-state region, its ticket / zero base / total in the header's pad words)
+        LprSpace scan{dfr.tcnt, dfr.toff, nullptr, nullptr, nullptr, nullptr, nullptr,
+                      reinterpret_cast<unsigned long long*>(ws + 1), 0u};
+        const unsigned scan_blocks = (unsigned)(((size_t)n_tiles + kBlock * kScanPer - 1) / (kBlock * kScanPer));
+        hipLaunchKernelGGL(lpr_scan_kernel, dim3(scan_blocks), dim3(kBlock), 0, st, scan, (size_t)n_tiles,
+                           (const unsigned long long*)&ws->pad[1], &ws->pad[2], ws,
+                           reinterpret_cast<unsigned*>(&ws->pad[0]));
+        HIP_TRY(hipGetLastError());
+        const size_t hl = heavy_lds_bytes(h->p, sizeof(T));
+        HIP_TRY(hipFuncSetAttribute((const void*)tile_heavy_write_kernel<T, IP, OP, OI, RL>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl));
+        hipLaunchKernelGGL((tile_heavy_write_kernel<T, IP, OP, OI, RL>), dim3(256), dim3(kBlock), hl, st, R, mag,
+                           (int)h->p, a->n_rows, (const IP*)a->indptr, a->indices, (const T*)a->data, (OP*)c->indptr,
+                           (OI*)c->indices, (T*)c->data, (unsigned long long)c->capacity, pl.caps, order, ws, dfr);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL((slot_copy_kernel<T, OP, OI>), dim3(std::min(n_tiles, kSlotCopyGrid)), dim3(kBlock), 0,
+                           st, dfr, pl.caps, a->n_rows, n_tiles, (OP*)c->indptr, (OI*)c->indices,
                            (T*)c->data, (unsigned long long)c->capacity);
         HIP_TRY(hipGetLastError());
     }

@@ -16,7 +16,7 @@ for L in "" ${LIBS:-}; do
 import csv, glob, sys
 for f in glob.glob(f"gpurun_out/ks_{sys.argv[1]}/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "lpr_" in r["Name"] or "spgemm" in r["Name"] or "defer" in r["Name"]:
+        if any(k in r["Name"] for k in ("lpr_", "spgemm", "defer", "slot_copy", "tile_heavy")):
             n = r["Name"].split("(")[0].split("<")[0].replace("void ", "").split("::")[-1]
             print(f"{n:28s} {r['Calls']:>5} {float(r['AverageNs'])/1e6:8.3f}")
 PY
