@@ -1314,7 +1314,7 @@ __device__ __forceinline__ bool lpr_bloom(const uint16_t* cb, uint32_t kst, uint
 
 // Exact repeat check of one row's slot range [kst, kst + n) (the staged wave kernel): every pair of
 // its first 16 columns compared in registers (120 compares, straight-line, no false alarms: ~1/3
-// of the Bloom check's VALU, which also flagged ~1% of the rows for nothing); a row of more than 16
+// of the round-5 3 x 64-bit Bloom check's VALU, which also flagged ~1% of the rows for nothing); a row of more than 16
 // products is flagged (the exact path handles it). Columns past n are distinct sentinels.
 __device__ __forceinline__ bool lpr_repeat16(const uint16_t* cb, uint32_t kst, uint32_t n, uint32_t lim) {
     uint32_t c[16];
