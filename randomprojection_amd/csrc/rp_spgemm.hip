@@ -623,12 +623,6 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     const uint4* pk4 = reinterpret_cast<const uint4*>(s_pkr);
                     const uint32_t gq = q >> 2, oq = q & 3u;
                     bool leader = true;
-#ifdef RP_PROBE_NOSTAGE2  // timing probe only (wrong results): every product leads its own group
-                    if (true) {
-                        s_rank[q] = 1;
-                        continue;
-                    }
-#endif
                     for (uint32_t g = rs >> 2; g < gq; ++g) {
                         const uint4 k4 = pk4[g];
                         leader &= (k4.x != kr) & (k4.y != kr) & (k4.z != kr) & (k4.w != kr);
@@ -668,12 +662,8 @@ spgemm_lookback_kernel(RL R, T mag, int p, int64_t n_rows, const IP* __restrict_
                     s_pool = (unsigned long long)tile * dfr.slot;
                 } else {
                     if (tid < 64) {
-#ifdef RP_PROBE_NOLOOKBACK  // timing probe only (wrong results): no look-back, every tile at 0
-                        if (tid == 0) s_off = 0;
-#else
                         const unsigned long long g = lookback_wave(states, tile, tile_c, ws, -1, true, 0);
                         if (tid == 0) s_off = g;
-#endif
                     }
                     __syncthreads();
                 }
