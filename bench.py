@@ -113,7 +113,7 @@ def step_kernels(plan, staged_run, call="sync"):
         if plan["staged"] == "auto":
             ks = ["lpr_choose_kernel"] + ks
         return ks
-    return ["spgemm_lookback_kernel", "defer_copy_kernel"]
+    return ["spgemm_lookback_kernel", "lpr_scan_kernel", "tile_heavy_write_kernel", "slot_copy_kernel"]
 
 
 def algorithmic_bytes_per_row(a, rbar, c):

@@ -8,6 +8,6 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 src = open(os.path.join(ROOT, "randomprojection_amd", "csrc", "rp_spgemm.hip")).read()
-old = "v[u] = (f >= lo && f < hi && hit) ? W32[wb | col] : 0u;"
+old = "w[u] = __builtin_amdgcn_raw_buffer_load_b32(wr, hit ? col * 4u : kOob, 0, 0);"
 assert src.count(old) == 1, "gather kernel changed: update the probe"
-open(sys.argv[1], "w").write(src.replace(old, "v[u] = (f >= lo && f < hi && hit) ? (wb | col) : 0u;"))
+open(sys.argv[1], "w").write(src.replace(old, "w[u] = hit ? col : 0u;"))

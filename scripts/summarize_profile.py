@@ -2,7 +2,7 @@
 
 One projection step = the kernels of rp_project_device: the row-lane pipeline (lpr_* kernels, the
 default for short rows over a packed R; staged: reserve/partition/gather + wave) or the tile
-pipeline (spgemm_lookback_kernel + defer_copy_kernel). Reads
+pipeline (spgemm_lookback_kernel + scan + tile_heavy_write_kernel + slot_copy_kernel). Reads
 gpurun_out/prof_<tag>_trace/*kernel_stats.csv and the separate PMC passes
 (gpurun_out/prof_<tag>_pmc_*/*counter_collection.csv) and writes
   profiles/<tag>_kernel_stats.csv      the rocprofv3 --stats summary (copied)
@@ -24,7 +24,7 @@ import os
 import shutil
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STEP_KERNELS = ("spgemm_lookback_kernel", "defer_copy_kernel",
+STEP_KERNELS = ("spgemm_lookback_kernel", "slot_copy_kernel", "tile_heavy_write_kernel",
                 "lpr_reserve_kernel", "lpr_partition_kernel", "lpr_gather_kernel", "lpr_wave_kernel",
                 "lpr_main_flat_kernel", "lpr_choose_kernel",
                 "lpr_heavy_count_kernel", "lpr_scan_kernel",
