@@ -342,6 +342,26 @@ def test_rowlane_staged_wave_edges(R2m_p1k):
     _check_rowlane_staged(R, sp.vstack([kdd_like(rng, 9 * 256 + 5, m, mean=11.2, values="normal")]).tocsr(), 19)
 
 
+def test_rowlane_staged_zero_values_and_empty_rows(R2m_p1k):
+    """Explicit zeros (+0.0 and -0.0, ~4% of the values, some rows all zero) among KDD-like rows
+    with empty rows between them: a zero value's products are not in the slot, so its row is
+    rebuilt by the wave kernel's exact path (rows flagged by their ordinal among the unit's
+    nonempty rows, mapped back to row lanes after the flat pass)."""
+    rng = np.random.default_rng(4040)
+    R = R2m_p1k
+    m = R.shape[0]
+    A = kdd_like(rng, 12 * 256 + 17, m, mean=11.2, values="normal").tolil()
+    A[rng.choice(A.shape[0], 400, replace=False)] = 0  # empty rows between nonempty ones
+    A = A.tocsr()
+    A.sort_indices()
+    z = rng.random(A.nnz) < 0.04
+    A.data[z] = np.where(rng.random(int(z.sum())) < 0.5, 0.0, -0.0).astype(np.float32)
+    for r in rng.choice(A.shape[0], 40, replace=False):  # rows of zeros only
+        A.data[A.indptr[r]:A.indptr[r + 1]] = 0.0
+    assert A.nnz == int(A.indptr[-1])  # the explicit zeros stay stored
+    _check_rowlane_staged(R, A, 16)
+
+
 @pytest.mark.parametrize("k", [15, 16, 17])
 def test_rowlane_staged_unit_cap(R2m_p1k, k):
     """Units at the wave kernel's register cap: 64 rows of k entries (k = 16: exactly 16 steps of 64
