@@ -946,22 +946,11 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
     __shared__ int s_over;
     __shared__ uint32_t s_gate;
     const int tid = threadIdx.x, q = tid >> 8, qt = tid & (kBlock - 1), w = tid >> 6;
-    // Another workgroup of this launch may clear the gate (segment overflow below) at any time, so
-    // the gate is read ONCE per workgroup and broadcast: every wave takes the same branch (a split
-    // workgroup would run the scan and the S stores with LDS state its exited waves never wrote).
-    if (tid == 0) s_gate = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (s_gate == 0) return;  // uniform
     const unsigned t0 = xcd_tile(blockIdx.x, s8) * kPartTiles;
     if (t0 >= n_tiles) return;  // uniform
     const unsigned t = t0 + q;
     const bool live = t < n_tiles;  // part-uniform
-    unsigned char* dyn = reinterpret_cast<unsigned char*>(s_key) + lpr_partition_keys_bytes(cap_a, nb);
-    uint32_t* s_cur = reinterpret_cast<uint32_t*>(dyn);  // per (tile, unit, bucket): the part's start in the layout
-    int64_t* s_dst = reinterpret_cast<int64_t*>(dyn + 16 * (size_t)kPartTiles * nb);  // per (tile, bucket)
-    uint16_t* s_st = reinterpret_cast<uint16_t*>(dyn + 24 * (size_t)kPartTiles * nb);  // per tile: nb + 1
-    uint8_t* s_bk = reinterpret_cast<uint8_t*>(dyn + 24 * (size_t)kPartTiles * nb +
-                                               ((2 * (size_t)kPartTiles * (nb + 1) + 15) & ~size_t(15)));
+    // the tile's row pointers are requested with the gate (one memory round trip for both)
     int64_t ea = 0, ne = 0;
     uint32_t u1 = 0, u2 = 0, u3 = 0;  // first entries of units 1..3 (tile-relative)
     if (live) {
@@ -972,6 +961,18 @@ lpr_partition_kernel(const IP* __restrict__ Ap, const int32_t* __restrict__ Aj, 
         u2 = (uint32_t)((int64_t)Ap[std::min<int64_t>(row0 + 128, n_rows)] - ea);
         u3 = (uint32_t)((int64_t)Ap[std::min<int64_t>(row0 + 192, n_rows)] - ea);
     }
+    // Another workgroup of this launch may clear the gate (segment overflow below) at any time, so
+    // the gate is read ONCE per workgroup and broadcast: every wave takes the same branch (a split
+    // workgroup would run the scan and the S stores with LDS state its exited waves never wrote).
+    if (tid == 0) s_gate = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_gate == 0) return;  // uniform
+    unsigned char* dyn = reinterpret_cast<unsigned char*>(s_key) + lpr_partition_keys_bytes(cap_a, nb);
+    uint32_t* s_cur = reinterpret_cast<uint32_t*>(dyn);  // per (tile, unit, bucket): the part's start in the layout
+    int64_t* s_dst = reinterpret_cast<int64_t*>(dyn + 16 * (size_t)kPartTiles * nb);  // per (tile, bucket)
+    uint16_t* s_st = reinterpret_cast<uint16_t*>(dyn + 24 * (size_t)kPartTiles * nb);  // per tile: nb + 1
+    uint8_t* s_bk = reinterpret_cast<uint8_t*>(dyn + 24 * (size_t)kPartTiles * nb +
+                                               ((2 * (size_t)kPartTiles * (nb + 1) + 15) & ~size_t(15)));
     const uint32_t n = ne > cap_a ? 0u : (uint32_t)ne;  // a heavy tile stages nothing: all runs empty
     const int32_t* __restrict__ Ajt = Aj + ea;
     int32_t jj[kMaxE];  // feature | unit << 27 (staging needs m <= 2^26), -1 past the tile
@@ -1864,16 +1865,24 @@ lpr_wave_kernel(PackedR R, T mag, int64_t n_rows, const IP* __restrict__ Ap, con
         const uint16_t* __restrict__ cu0 = u ? cu1 - stg.ostride : cu1;
         const uint32_t* __restrict__ o2 = stg.off2 + (size_t)tile * stg.ostride;
         const int64_t* __restrict__ gbq = stg.gb + gq;
+        // unit 0 has no row before it: its c0 is masked to 0 after an unconditional load (an opaque
+        // mask: a select of a load becomes a branch around it, and the branch a wait)
+        uint32_t m0 = u ? 0xffffffffu : 0u;
+        __asm__("" : "+v"(m0));
 #pragma unroll
         for (int h = 0; h < kNBL; ++h) {
             const int b = std::min(64 * h + lane, stg.nb - 1);
-            const uint32_t c1 = cu1[b], c0 = u ? (uint32_t)cu0[b] : 0u;
+            const uint32_t c1 = cu1[b], c0 = (uint32_t)cu0[b] & m0;
             const bool ok = 64 * h + lane < stg.nb;
             cnt[h] = ok ? c1 - c0 : 0u;
             src[h] = (uint32_t)(gbq[b] - g0) + o2[b] + c0;
         }
     }
     const uint32_t staged = *stg.gate;  // uniform: 0 after a segment overflow (direct gathers)
+    // keep the table and gate loads here, in the row pointers' round trip: the compiler sank them
+    // below the early returns (they are only used on the staged path), which cost the unit one or
+    // two more dependent round trips before its S/D loads (wave kernel 6.59 -> 6.34 ms)
+    __asm__ volatile("" ::: "memory");
     const uint32_t nu = E1 - E0, nsteps = (nu + 63) >> 6;
     if (tn > cap_a || nu > ucap) {  // uniform: the partition staged nothing / too many for the registers
         go_heavy();
