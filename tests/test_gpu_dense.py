@@ -96,3 +96,31 @@ def test_side_stream_waits_for_casts(compute):
     got = dense_project_device(X, C, compute=compute, stream=side.cuda_stream)
     side.synchronize()
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_configs4_width_million_rows(compute):
+    """configs[4]'s full m x p (16384 -> 1024) on 1,000,003 device-resident rows (64 GB of f32 X;
+    the 10M-row pass itself is 655 GB and streams from the host): ONE librp GEMM launch over every
+    row, each 65,536-row block (the ragged last one included) against a chunked fp64 torch product
+    of the same (bf16-rounded for "bf16") operands, normwise within the north-star 1e-5."""
+    import torch
+    from randomprojection_amd.gaussian import dense_project_device, prepare_operand
+
+    n, m, p = 1_000_003, 16384, 1024
+    g = torch.Generator(device="cuda").manual_seed(4)
+    X = torch.randn(n, m, device="cuda", dtype=torch.float32, generator=g)
+    C = torch.randn(p, m, device="cuda", dtype=torch.float32, generator=g) / 128.0
+    Cc = prepare_operand(C, compute)
+    Y = dense_project_device(X, Cc, compute=compute, prepared_c=True)
+    assert Y.shape == (n, p) and Y.dtype == torch.float32
+    dt = torch.bfloat16 if compute == "bf16" else torch.float32
+    Cd = C.to(dt).double()
+    worst = 0.0
+    for s in range(0, n, 65536):
+        e = min(n, s + 65536)
+        ref = X[s:e].to(dt).double() @ Cd.T
+        rel = float(torch.linalg.norm(Y[s:e].double() - ref) / torch.linalg.norm(ref))
+        worst = max(worst, rel)
+        del ref
+    assert bool(torch.isfinite(Y).all()) and worst < 1e-5, worst
