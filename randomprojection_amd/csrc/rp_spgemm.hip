@@ -1330,6 +1330,10 @@ __device__ __forceinline__ bool lpr_repeat16(const uint16_t* cb, uint32_t kst, u
 // a slot with gaps (entries the exact path merged or dropped) is stored as built, and the copy
 // kernel finds each output's row and reverses it there. Both kernels apply the same test
 // (lpr_slot_final).
+// unit slots hold a multiple of 64 entries (whole 128-B lines of columns and of values) and are
+// stored as whole lines (the padding past the kept entries included): no line of a slot is written
+// partially (14.25-14.31 -> 14.14-14.22 ms per configs[1] pass, same box)
+constexpr uint32_t kSlotRound = 64u;
 __device__ __forceinline__ bool lpr_slot_final(uint32_t c, uint32_t kst, uint32_t pre) {
     return __ballot(c > 0 && kst != pre) == 0;
 }
@@ -1356,16 +1360,18 @@ __device__ __forceinline__ uint32_t lpr_store_slot(uint16_t* cb, T* vb, uint32_t
         __builtin_amdgcn_wave_barrier();
     }
     // 16 bytes per lane and store (8 columns, 16 / sizeof(T) values), non-temporal. A wave's slot
-    // regions start 16-B aligned and hold slot (a multiple of 32) entries: the rounded-up tail
-    // stays inside them.
+    // regions start 128-B aligned and hold slot (a multiple of 64) entries: the tail rounded up to
+    // whole lines stays inside them (extent <= slot: a fuller unit went heavy before its store).
     if (valid) rowmeta[lane] = kst | (c << 16);
     if (lane == 0) *cnt = tot;
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)oc, (short)0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)ov, (short)0, 0x7fffffff, 0x00020000);
-    for (uint32_t o = 8 * lane; o < extent; o += 512)
+    const uint32_t ext_c = (extent + 63) & ~63u;  // whole 128-B lines (the slot holds a multiple of 64 entries)
+    const uint32_t ext_v = (extent + 128u / (uint32_t)sizeof(T) - 1u) & ~(128u / (uint32_t)sizeof(T) - 1u);
+    for (uint32_t o = 8 * lane; o < ext_c; o += 512)
         __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u*>(cb + o), rc, 2 * o, 0, kAuxNT);
     constexpr uint32_t kPer = 16 / sizeof(T);
-    for (uint32_t o = kPer * lane; o < extent; o += 64 * kPer)
+    for (uint32_t o = kPer * lane; o < ext_v; o += 64 * kPer)
         __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u*>(vb + o), rv, (uint32_t)sizeof(T) * o, 0,
                                                kAuxNT);
     return tot;
@@ -2699,7 +2705,7 @@ Plan make_plan(const rp_projector* h, int64_t n_rows, int64_t nnz_a, bool allow_
         const double prods_w = std::max(1.0, avg * 64 * ppe);  // one wave's slot: 64 rows
         // mean + 7 sigma (sigma ~ 1.25 sqrt(mean) for single-magnitude SRP rows) + 32: KDD2012 608,
         // which keeps a tile's LDS (descriptors + the 4 slots) at 32 KB: 5 tiles per CU
-        pl.lpr_slot = (uint32_t)std::min<double>(65535.0, ((int)(prods_w + 8.75 * std::sqrt(prods_w) + 32.0) + 31) & ~31);
+        pl.lpr_slot = (uint32_t)std::min<double>(65472.0, ((int)(prods_w + 8.75 * std::sqrt(prods_w) + 32.0) + kSlotRound - 1) & ~(kSlotRound - 1));
         pl.lpr_chunk = std::min<int64_t>(n_rows, lpr_chunk_rows(h));
         pl.n_tiles = (pl.lpr_chunk + kLprRows - 1) / kLprRows;
         const size_t nw = 4 * (size_t)pl.n_tiles;

@@ -1,10 +1,15 @@
+#!/bin/bash
+# Round-6 final build (whole-line unit slots): PMC session keyed to the build (summarised on the box so
+# the bench line reads its traffic), the default bench line, the whole -m gpu suite.
 set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests/test_gpu_staged.py tests/test_gpu_parity.py tests/test_gpu_stream.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r06e_tests.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/r06e_tests.log; exit 1; }
-tail -2 gpurun_out/r06e_tests.log
-for o in fused_copy=-1 fused_copy=0 fused_copy=-1 fused_copy=0; do
-  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --host-steps 0 --option $o > gpurun_out/r06e_b.json 2>gpurun_out/r06e_b.err || { tail -5 gpurun_out/r06e_b.err; exit 7; }
-  python3 -c "import json; d=json.loads(open('gpurun_out/r06e_b.json').read().strip().splitlines()[-1]); print('$o', round(d['ms_per_step'],3), d['verified']['sample_bitexact_vs_oracle'], d['verified']['indptr_ok'], d['verified']['columns_ok'])"
-done
-BENCH="--option fused_copy=-1" bash scripts/gpu_kstats.sh > gpurun_out/r06e_kstats.txt 2>&1; cat gpurun_out/r06e_kstats.txt
+TAG=r06e SKIP_BENCH=1 PROF_ARGS="--steps 5 --warmup 2 --no-cpu-baseline --host-steps 0" bash scripts/gpu_profile.sh > gpurun_out/r06e_prof.log 2>&1 || { tail -5 gpurun_out/r06e_prof.log; exit 4; }
+echo prof-done
+timeout -k 10 500 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r06e_bench.json 2> gpurun_out/r06e_bench.err || { tail -5 gpurun_out/r06e_bench.err; exit 5; }
+tail -c 300 gpurun_out/r06e_bench.json; echo
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/r06e_gpu_tests.log 2>&1; rc=$?
+tail -3 gpurun_out/r06e_gpu_tests.log
+grep -E "PASSED|FAILED|ERROR" gpurun_out/r06e_gpu_tests.log | grep -v PASSED | head -20
+exit $rc
